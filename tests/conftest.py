@@ -1,0 +1,28 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
+
+
+def load_golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def ragged_cell(d, c, xkey='x', ykey='y', okey='offs'):
+    a, b = int(d[okey][c]), int(d[okey][c + 1])
+    return d[xkey][a:b].reshape(-1, 3), d[ykey][a:b]
+
+
+@pytest.fixture(scope='session')
+def golden():
+    return load_golden
