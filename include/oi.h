@@ -1,0 +1,112 @@
+/* liboi -- MI355X-native per-grid-cell full-GP regression (C ABI).
+ *
+ * Drop-in boundary for the hot path of William-gregory/OptimalInterpolation,
+ * 2021_paper_production/GPR_CS2S3.py (abbreviated GPR: below):
+ *
+ *   oi_gpr_batch        replaces the per-cell loops GPR:258-261 (pass 1,
+ *                       GPR3D(index) with opt=True) and GPR:316-319 (pass 2,
+ *                       GPR3D(index, opt=False)): one call fits / predicts a
+ *                       ragged batch of cells.  Per cell it computes exactly
+ *                       what GPR3D (GPR:143-191) returns.
+ *   oi_nlml_grad_batch  replaces SMLII (GPR:107-141) for a batch of cells at
+ *                       given log-hyper-parameters.
+ *   oi_cg_*             the host optimiser on its own: scipy's
+ *                       minimize(method='CG', jac=True) as called at GPR:166,
+ *                       driven by caller-supplied objective values.
+ *
+ * Conventions: plain host pointers, row-major arrays, fp64 throughout.  The
+ * library owns all device memory.  Functions return 0 on success or a
+ * negative OI_E* code (API misuse / HIP failure; message via oi_last_error).
+ * Per-cell numerical failure is NOT an error: as in GPR:139-140 and
+ * GPR:187-191, a non-positive-definite covariance gives nlZ = +inf / gradient
+ * +inf (objective) or NaN outputs (GPR3D), with status[c] = 1.
+ * A cell with zero observations is valid (GPR3D returns (mean, sqrt(sf2), -0, ...)).
+ */
+#ifndef OI_H
+#define OI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OI_VERSION 1
+
+#define OI_E_ARG (-1)    /* invalid argument */
+#define OI_E_HIP (-2)    /* HIP runtime / kernel launch failure */
+#define OI_E_NOMEM (-3)  /* a single cell does not fit the device workspace */
+#define OI_E_NODEV (-4)  /* no usable GPU */
+
+typedef struct oi_options {
+  int32_t device;      /* HIP device ordinal (default 0) */
+  int32_t maxiter;     /* CG maxiter; <0 => len(x0)*200 = 1200 (scipy default) */
+  double gtol;         /* CG gradient tolerance (scipy default 1e-5) */
+  void* stream;        /* hipStream_t to launch on; NULL => the library's stream */
+  int64_t pool_bytes;  /* device workspace budget; 0 => 60% of free HBM */
+  int32_t max_pool;    /* max cells resident at once; 0 => automatic */
+  int32_t profile;     /* 1 => record per-kernel HIP-event timings (oi_profile_json) */
+} oi_options;
+
+/* Fill *o with defaults. */
+void oi_options_default(oi_options* o);
+
+/* Per-cell GP regression for a ragged batch (GPR3D semantics, GPR:143-191).
+ *   xyt    [N x 3]  neighbour inputs (x [m], y [m], t [day]) of all cells,
+ *                   cell c owning rows offs[c] .. offs[c+1]-1, in the order
+ *                   the caller's neighbour query returned them (GPR:159-160)
+ *   z      [N]      observations (GPR:161)
+ *   offs   [ncell+1] row offsets, offs[0] = 0, non-decreasing
+ *   xs     [ncell x 3] prediction targets (cx, cy, T_mid)  (GPR:164)
+ *   mean   prior mean (GPR:212); mX = mean * ones(n)      (GPR:163)
+ *   x0     [6] initial log-hyper-parameters (GPR:217); used when opt != 0
+ *   opt    1: fit hypers by CG then predict (GPR:166-168)
+ *          0: predict with given hypers hyp (GPR:170-172)
+ *   hyp    [ncell x 5] (lx, ly, lt, sf2, sn2) when opt == 0, else NULL
+ *   out    [ncell x 8] (fs, sd, lZ, lx, ly, lt, sf2, sn2); for opt == 0
+ *                   only fs, sd, lZ are meaningful (hyp echoed in 3..7)
+ *   status [ncell]   0 ok, 1 covariance not positive definite (NaN outputs)
+ *   info   [ncell x 4] or NULL: (nit, cg_status, nfev, n_objective_evals)
+ */
+int oi_gpr_batch(const double* xyt, const double* z, const int64_t* offs, int64_t ncell,
+                 const double* xs, double mean, const double* x0, int32_t opt,
+                 const double* hyp, double* out, int32_t* status, int32_t* info,
+                 const oi_options* opts);
+
+/* SMLII (GPR:107-141) for a batch of cells at fixed log-hypers.
+ *   xyt, offs as above; y [N] outputs; mX [N] prior mean per observation
+ *   h   [ncell x 6] log-hypers (lx, ly, lt, sf2, sn2, unused)
+ *   nlz [ncell] ; grad [ncell x 6] (reference gradient incl. its factor-2
+ *   components 3 and 4 and the zero 6th component); status [ncell] or NULL
+ */
+int oi_nlml_grad_batch(const double* xyt, const double* y, const double* mX,
+                       const int64_t* offs, int64_t ncell, const double* h, double* nlz,
+                       double* grad, int32_t* status, const oi_options* opts);
+
+/* ---- host optimiser (scipy 1.15 CG restated; see csrc/cg.hpp) ---- */
+typedef struct oi_cg oi_cg;
+/* x0: 6 log-hypers. gtol/maxiter as in oi_options (maxiter < 0 => 1200). */
+oi_cg* oi_cg_create(const double* x0, double gtol, int32_t maxiter);
+/* Advance until the optimiser needs an objective value: returns 1 and writes
+ * the requested point to x_req[6]; returns 0 when finished; <0 on misuse. */
+int oi_cg_step(oi_cg* h, double* x_req);
+/* Supply f and g[6] at the last requested point. */
+int oi_cg_feed(oi_cg* h, double f, const double* g);
+/* Result after oi_cg_step returned 0: x[6], fun, nit, status (scipy codes),
+ * nfev/njev (scipy counters) and nobj (objective evaluations made). */
+int oi_cg_result(oi_cg* h, double* x, double* fun, int32_t* nit, int32_t* status,
+                 int64_t* nfev, int64_t* njev, int64_t* nobj);
+void oi_cg_destroy(oi_cg* h);
+
+/* ---- diagnostics ---- */
+const char* oi_last_error(void);  /* thread-local message of the last failure */
+int32_t oi_version(void);
+/* JSON with per-kernel {launches, total_ms, flops} since the last reset
+ * (requires opts.profile=1 on the timed calls). Returns bytes needed. */
+int64_t oi_profile_json(char* buf, int64_t len);
+void oi_profile_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OI_H */

@@ -1,0 +1,217 @@
+"""ctypes binding of liboi.so (include/oi.h).
+
+The shared library is built in-tree by ``make -C optimalinterpolation_amd``
+(or ``__graft_entry__.build()``).  It is the product path: there is no CPU
+fallback, and every entry point raises if the library or a GPU is missing.
+
+PyTorch is imported first (when present) so that liboi.so binds to the same
+HIP runtime instance that torch already loaded (both carry the soname
+libamdhip64.so.7); streams handed over from torch are then valid here.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+try:  # plumbing only: share torch's HIP runtime if torch is in the process
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'liboi.so')
+
+_lib = None
+_lock = threading.Lock()
+
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_int64_p = ctypes.POINTER(ctypes.c_int64)
+c_int32_p = ctypes.POINTER(ctypes.c_int32)
+
+# every symbol include/oi.h declares (tests/test_abi.py checks the export list)
+EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_create',
+           'oi_cg_step', 'oi_cg_feed', 'oi_cg_result', 'oi_cg_destroy', 'oi_last_error',
+           'oi_version', 'oi_profile_json', 'oi_profile_reset')
+
+
+class OiOptions(ctypes.Structure):
+    _fields_ = [('device', ctypes.c_int32), ('maxiter', ctypes.c_int32), ('gtol', ctypes.c_double),
+                ('stream', ctypes.c_void_p), ('pool_bytes', ctypes.c_int64),
+                ('max_pool', ctypes.c_int32), ('profile', ctypes.c_int32)]
+
+
+class OiError(RuntimeError):
+    pass
+
+
+def load():
+    """Load liboi.so (once).  Raises OiError when it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise OiError(f"{LIB_PATH} not built: run `make -C {_HERE}` (or __graft_entry__.build())")
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.oi_options_default.argtypes = [ctypes.POINTER(OiOptions)]
+        lib.oi_options_default.restype = None
+        lib.oi_gpr_batch.argtypes = [c_double_p, c_double_p, c_int64_p, ctypes.c_int64, c_double_p,
+                                     ctypes.c_double, c_double_p, ctypes.c_int32, c_double_p,
+                                     c_double_p, c_int32_p, c_int32_p, ctypes.POINTER(OiOptions)]
+        lib.oi_gpr_batch.restype = ctypes.c_int
+        lib.oi_nlml_grad_batch.argtypes = [c_double_p, c_double_p, c_double_p, c_int64_p,
+                                           ctypes.c_int64, c_double_p, c_double_p, c_double_p,
+                                           c_int32_p, ctypes.POINTER(OiOptions)]
+        lib.oi_nlml_grad_batch.restype = ctypes.c_int
+        lib.oi_cg_create.argtypes = [c_double_p, ctypes.c_double, ctypes.c_int32]
+        lib.oi_cg_create.restype = ctypes.c_void_p
+        lib.oi_cg_step.argtypes = [ctypes.c_void_p, c_double_p]
+        lib.oi_cg_step.restype = ctypes.c_int
+        lib.oi_cg_feed.argtypes = [ctypes.c_void_p, ctypes.c_double, c_double_p]
+        lib.oi_cg_feed.restype = ctypes.c_int
+        lib.oi_cg_result.argtypes = [ctypes.c_void_p, c_double_p, c_double_p, c_int32_p, c_int32_p,
+                                     c_int64_p, c_int64_p, c_int64_p]
+        lib.oi_cg_result.restype = ctypes.c_int
+        lib.oi_cg_destroy.argtypes = [ctypes.c_void_p]
+        lib.oi_cg_destroy.restype = None
+        lib.oi_last_error.argtypes = []
+        lib.oi_last_error.restype = ctypes.c_char_p
+        lib.oi_version.argtypes = []
+        lib.oi_version.restype = ctypes.c_int32
+        lib.oi_profile_json.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+        lib.oi_profile_json.restype = ctypes.c_int64
+        lib.oi_profile_reset.argtypes = []
+        lib.oi_profile_reset.restype = None
+        _lib = lib
+        return lib
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(ctypes.POINTER(ctype)) if a is not None else None
+
+
+def _check(rc):
+    if rc != 0:
+        raise OiError(f"liboi error {rc}: {load().oi_last_error().decode(errors='replace')}")
+
+
+def options(device=0, maxiter=-1, gtol=1e-5, stream=None, pool_bytes=0, max_pool=0, profile=False):
+    o = OiOptions()
+    load().oi_options_default(ctypes.byref(o))
+    o.device = int(device)
+    o.maxiter = int(maxiter)
+    o.gtol = float(gtol)
+    o.stream = stream
+    o.pool_bytes = int(pool_bytes)
+    o.max_pool = int(max_pool)
+    o.profile = 1 if profile else 0
+    return o
+
+
+def gpr_batch(xyt, z, offs, xs, mean, x0=None, opt=True, hyp=None, info=False, **opt_kw):
+    """oi_gpr_batch: returns (out [ncell x 8], status [ncell], info [ncell x 4] or None)."""
+    lib = load()
+    xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+    z = np.ascontiguousarray(z, dtype=np.float64)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1, 3)
+    ncell = len(offs) - 1
+    if xs.shape[0] != ncell or offs[0] != 0 or offs[-1] != len(z) or xyt.shape[0] != len(z):
+        raise ValueError("inconsistent ragged batch")
+    out = np.empty((ncell, 8))
+    status = np.zeros(ncell, dtype=np.int32)
+    inf = np.zeros((ncell, 4), dtype=np.int32) if info else None
+    x0a = np.ascontiguousarray(x0, dtype=np.float64) if x0 is not None else None
+    hypa = np.ascontiguousarray(hyp, dtype=np.float64).reshape(-1, 5) if hyp is not None else None
+    if opt and (x0a is None or x0a.shape != (6,)):
+        raise ValueError("opt=True needs x0 of length 6")
+    if not opt and (hypa is None or hypa.shape[0] != ncell):
+        raise ValueError("opt=False needs hyp [ncell x 5]")
+    o = options(**opt_kw)
+    rc = lib.oi_gpr_batch(_ptr(xyt, ctypes.c_double), _ptr(z, ctypes.c_double),
+                          _ptr(offs, ctypes.c_int64), ncell, _ptr(xs, ctypes.c_double),
+                          float(mean), _ptr(x0a, ctypes.c_double), 1 if opt else 0,
+                          _ptr(hypa, ctypes.c_double), _ptr(out, ctypes.c_double),
+                          _ptr(status, ctypes.c_int32), _ptr(inf, ctypes.c_int32), ctypes.byref(o))
+    _check(rc)
+    return out, status, inf
+
+
+def nlml_grad_batch(xyt, y, mX, offs, h, **opt_kw):
+    """oi_nlml_grad_batch: returns (nlz [ncell], grad [ncell x 6], status [ncell])."""
+    lib = load()
+    xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    mX = np.ascontiguousarray(mX, dtype=np.float64)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    h = np.ascontiguousarray(h, dtype=np.float64).reshape(-1, 6)
+    ncell = len(offs) - 1
+    if h.shape[0] != ncell or offs[-1] != len(y) or len(mX) != len(y) or xyt.shape[0] != len(y):
+        raise ValueError("inconsistent ragged batch")
+    nlz = np.empty(ncell)
+    grad = np.empty((ncell, 6))
+    status = np.zeros(ncell, dtype=np.int32)
+    o = options(**opt_kw)
+    rc = lib.oi_nlml_grad_batch(_ptr(xyt, ctypes.c_double), _ptr(y, ctypes.c_double),
+                                _ptr(mX, ctypes.c_double), _ptr(offs, ctypes.c_int64), ncell,
+                                _ptr(h, ctypes.c_double), _ptr(nlz, ctypes.c_double),
+                                _ptr(grad, ctypes.c_double), _ptr(status, ctypes.c_int32),
+                                ctypes.byref(o))
+    _check(rc)
+    return nlz, grad, status
+
+
+class CG:
+    """The host optimiser (scipy CG restated in C++), driven from Python."""
+
+    def __init__(self, x0, gtol=1e-5, maxiter=-1):
+        self._lib = load()
+        x0 = np.ascontiguousarray(x0, dtype=np.float64)
+        self._h = self._lib.oi_cg_create(_ptr(x0, ctypes.c_double), float(gtol), int(maxiter))
+        if not self._h:
+            raise OiError(self._lib.oi_last_error().decode())
+        self._x = np.empty(6)
+
+    def step(self):
+        """None when finished, else the point (6,) whose f, g are needed."""
+        rc = self._lib.oi_cg_step(self._h, _ptr(self._x, ctypes.c_double))
+        if rc < 0:
+            _check(rc)
+        return None if rc == 0 else self._x.copy()
+
+    def feed(self, f, g):
+        g = np.ascontiguousarray(g, dtype=np.float64)
+        _check(self._lib.oi_cg_feed(self._h, float(f), _ptr(g, ctypes.c_double)))
+
+    def result(self):
+        x = np.empty(6)
+        fun = ctypes.c_double()
+        nit = ctypes.c_int32()
+        st = ctypes.c_int32()
+        nfev = ctypes.c_int64()
+        njev = ctypes.c_int64()
+        nobj = ctypes.c_int64()
+        _check(self._lib.oi_cg_result(self._h, _ptr(x, ctypes.c_double), ctypes.byref(fun),
+                                      ctypes.byref(nit), ctypes.byref(st), ctypes.byref(nfev),
+                                      ctypes.byref(njev), ctypes.byref(nobj)))
+        return dict(x=x, fun=fun.value, nit=nit.value, status=st.value, nfev=nfev.value,
+                    njev=njev.value, nobj=nobj.value)
+
+    def __del__(self):
+        if getattr(self, '_h', None):
+            self._lib.oi_cg_destroy(self._h)
+            self._h = None
+
+
+def profile_json():
+    import json
+    lib = load()
+    n = lib.oi_profile_json(None, 0)
+    buf = ctypes.create_string_buffer(int(n))
+    lib.oi_profile_json(buf, n)
+    return json.loads(buf.value.decode())
+
+
+def profile_reset():
+    load().oi_profile_reset()

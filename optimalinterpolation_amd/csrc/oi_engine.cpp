@@ -1,0 +1,735 @@
+// liboi host engine: the C ABI of include/oi.h.
+//
+// Continuous batching of independent grid cells on one GPU:
+//   * every cell owns a region of a device arena (packed tiles, vectors,
+//     partial sums) for as long as it is resident;
+//   * a fitting cell runs scipy's CG (cg.hpp) as a coroutine that suspends
+//     whenever it needs SMLII at a new point;
+//   * one "round" = one launch sequence that evaluates SMLII for every
+//     suspended cell and the GPR3D predict block for every cell whose fit
+//     has finished; then results come back, coroutines resume, finished
+//     cells leave and queued cells (largest n first) take their place.
+// Per-cell arithmetic never depends on which other cells share a round.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/oi.h"
+#include "cg.hpp"
+#include "oi_device.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIPC(expr)                                                                            \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      throw HipError(std::string(#expr) + ": " + hipGetErrorString(e_));                      \
+  } while (0)
+
+struct HipError {
+  std::string msg;
+  explicit HipError(std::string m) : msg(std::move(m)) {}
+};
+
+inline int tiles_of(int64_t n) { return (int)((n + OI_NB - 1) / OI_NB); }
+
+// ------------------------------------------------------------- arena
+// First-fit free list over one device allocation (256-byte granules).
+class Arena {
+ public:
+  void init(size_t bytes) {
+    HIPC(hipMalloc(&base_, bytes));
+    size_ = bytes;
+    free_.clear();
+    free_[0] = bytes;
+  }
+  ~Arena() {
+    if (base_) (void)hipFree(base_);
+  }
+  size_t size() const { return size_; }
+  // returns offset or SIZE_MAX
+  size_t alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~size_t(255);
+    for (auto it = free_.begin(); it != free_.end(); ++it) {
+      if (it->second >= bytes) {
+        size_t off = it->first, len = it->second;
+        free_.erase(it);
+        if (len > bytes) free_[off + bytes] = len - bytes;
+        return off;
+      }
+    }
+    return SIZE_MAX;
+  }
+  void release(size_t off, size_t bytes) {
+    bytes = (bytes + 255) & ~size_t(255);
+    auto it = free_.emplace(off, bytes).first;
+    auto nx = std::next(it);
+    if (nx != free_.end() && it->first + it->second == nx->first) {
+      it->second += nx->second;
+      free_.erase(nx);
+    }
+    if (it != free_.begin()) {
+      auto pv = std::prev(it);
+      if (pv->first + pv->second == it->first) {
+        pv->second += it->second;
+        free_.erase(it);
+      }
+    }
+  }
+  char* ptr(size_t off) const { return static_cast<char*>(base_) + off; }
+
+ private:
+  void* base_ = nullptr;
+  size_t size_ = 0;
+  std::map<size_t, size_t> free_;
+};
+
+size_t cell_bytes(int64_t n, bool eval) {
+  const size_t T = (size_t)tiles_of(n), nt = T * (T + 1) / 2;
+  size_t b = 0;
+  auto add = [&](size_t x) { b += (x + 255) & ~size_t(255); };
+  add(nt * OI_TILE * 8);                         // L
+  if (eval) add(nt * OI_TILE * 8);               // W
+  add(T * OI_TILE * 8);                          // Dinv
+  add(4 * T * OI_NB * 8);                        // vec
+  add((size_t)OI_PART_SIZE(nt, T) * 8);          // part
+  return b;
+}
+
+// ------------------------------------------------------------- profiling
+enum KernelId { K_BUILD, K_CHOL, K_TRSM, K_ZVEC, K_AVEC, K_LAUUM, K_FINAL, K_PRED, K_COUNT };
+const char* kKernelName[K_COUNT] = {"k_build",  "k_chol_update", "k_trsm_trtri", "k_zvec",
+                                    "k_avec",   "k_lauum_grad",  "k_finalize",   "k_predict"};
+struct KStat {
+  int64_t launches = 0;
+  double ms = 0.0;
+  double flops = 0.0;  // executed tile-GEMM flops (2*64^3 per tile product)
+};
+std::mutex g_prof_mu;
+KStat g_prof[K_COUNT];
+struct RunStat {
+  int64_t rounds = 0, evals = 0, predicts = 0;
+  double wall_s = 0.0;
+} g_run;
+
+// ------------------------------------------------------------- context
+struct Context {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  Arena arena;
+  size_t arena_bytes = 0;
+  std::mutex mu;
+};
+
+std::mutex g_ctx_mu;
+std::map<int, std::unique_ptr<Context>> g_ctx;
+
+Context& context(int device, int64_t pool_bytes) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto& p = g_ctx[device];
+  if (!p) {
+    p = std::make_unique<Context>();
+    p->device = device;
+    HIPC(hipSetDevice(device));
+    HIPC(hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking));
+  }
+  HIPC(hipSetDevice(device));
+  size_t want = (size_t)pool_bytes;
+  if (want == 0) {
+    if (p->arena_bytes) return *p;  // keep the automatic arena between calls
+    size_t fr = 0, tot = 0;
+    HIPC(hipMemGetInfo(&fr, &tot));
+    want = (size_t)(fr * 0.6);
+  }
+  if (want != p->arena_bytes) {
+    p->arena.~Arena();
+    new (&p->arena) Arena();
+    p->arena.init(want);
+    p->arena_bytes = want;
+  }
+  return *p;
+}
+
+// device buffer RAII
+struct DBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  void reserve(size_t bytes) {
+    if (bytes <= n) return;
+    if (p) HIPC(hipFree(p));
+    p = nullptr;
+    HIPC(hipMalloc(&p, bytes));
+    n = bytes;
+  }
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+struct HBuf {  // pinned host
+  void* p = nullptr;
+  size_t n = 0;
+  void reserve(size_t bytes) {
+    if (bytes <= n) return;
+    if (p) HIPC(hipHostFree(p));
+    p = nullptr;
+    HIPC(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    n = bytes;
+  }
+  ~HBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+// ------------------------------------------------------------- the batch
+struct Job {
+  // inputs (host)
+  const double* xyt;
+  const int64_t* offs;
+  int64_t ncell;
+  std::vector<double> r;        // y - mX
+  const double* xs = nullptr;   // ncell x 3 (predict)
+  double mean = 0.0;
+  // per-cell work description
+  enum Kind { FIT_PREDICT, PREDICT_ONLY, EVAL_ONLY } kind;
+  const double* x0 = nullptr;
+  const double* hyp = nullptr;  // PREDICT_ONLY: ncell x 5
+  const double* h = nullptr;    // EVAL_ONLY: ncell x 6
+  oi::CgOptions cg;
+  // outputs
+  double* out = nullptr;        // FIT/PRED: ncell x 8
+  int32_t* status = nullptr;
+  int32_t* info = nullptr;
+  double* nlz = nullptr;        // EVAL_ONLY
+  double* grad = nullptr;
+};
+
+struct Slot {
+  int64_t cell = -1;
+  size_t off = 0, bytes = 0;
+  int phase = 0;  // 0 fit (eval), 1 predict, 2 eval-only
+  oi::EvalSlot mail;
+  oi::Task<oi::CgResult> task;
+  double hyp[5] = {0, 0, 0, 0, 0};
+  oi::CgResult res;
+};
+
+int run(const Job& job, const oi_options& o) {
+  auto t_start = std::chrono::steady_clock::now();
+  Context& ctx = context(o.device, o.pool_bytes);
+  std::lock_guard<std::mutex> lk(ctx.mu);
+  HIPC(hipSetDevice(ctx.device));
+  hipStream_t st = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
+  const int64_t ncell = job.ncell;
+  const int64_t N = job.offs[ncell];
+
+  // inputs to device once
+  DBuf d_xyt, d_r;
+  d_xyt.reserve(std::max<size_t>(N * 3 * 8, 256));
+  d_r.reserve(std::max<size_t>(N * 8, 256));
+  if (N > 0) {
+    HIPC(hipMemcpyAsync(d_xyt.p, job.xyt, N * 3 * 8, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_r.p, job.r.data(), N * 8, hipMemcpyHostToDevice, st));
+  }
+  const bool eval_mem = job.kind != Job::PREDICT_ONLY;
+
+  // admission order: largest cells first (cost ~ n^3), ties by index
+  std::vector<int64_t> order(ncell);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    return job.offs[a + 1] - job.offs[a] > job.offs[b + 1] - job.offs[b];
+  });
+  size_t max_cell = 0;
+  for (int64_t c = 0; c < ncell; ++c)
+    max_cell = std::max(max_cell, cell_bytes(job.offs[c + 1] - job.offs[c], eval_mem));
+  if (max_cell > ctx.arena.size())
+    return fail(OI_E_NOMEM, "a cell needs " + std::to_string(max_cell) + " bytes of workspace, pool is " +
+                                std::to_string(ctx.arena.size()));
+
+  const int cap = (int)std::min<int64_t>(ncell, o.max_pool > 0 ? o.max_pool : 2048);
+  std::vector<Slot> slots(cap);
+  std::vector<int> free_slots;
+  for (int s = cap - 1; s >= 0; --s) free_slots.push_back(s);
+  std::vector<int> active;
+
+  DBuf d_cells, d_list, d_res, d_stat;
+  HBuf h_cells, h_list, h_res, h_stat;
+  d_cells.reserve(cap * sizeof(OiCell));
+  h_cells.reserve(cap * sizeof(OiCell));
+  d_list.reserve(cap * 4 * 3);
+  h_list.reserve(cap * 4 * 3);
+  d_res.reserve(cap * OI_OUT_N * 8);
+  h_res.reserve(cap * OI_OUT_N * 8);
+  d_stat.reserve(cap * 4);
+  h_stat.reserve(cap * 4);
+  OiCell* hc = (OiCell*)h_cells.p;
+  const OiCell* dc = (const OiCell*)d_cells.p;
+  int32_t* hl = (int32_t*)h_list.p;
+  int32_t* dl = (int32_t*)d_list.p;
+  double* hres = (double*)h_res.p;
+  int32_t* hst = (int32_t*)h_stat.p;
+
+  // profiling: one start/stop event pair per launch of a round
+  std::vector<hipEvent_t> ev;
+  std::vector<int> ev_kind;
+  if (o.profile) {
+    ev.resize(2 * (2 * 1024 + 16));
+    for (auto& e : ev) HIPC(hipEventCreate(&e));
+  }
+  double kms[K_COUNT] = {0}, kfl[K_COUNT] = {0};
+  int64_t kln[K_COUNT] = {0};
+
+  size_t next = 0;
+  int64_t rounds = 0, evals = 0, predicts = 0;
+  while (next < order.size() || !active.empty()) {
+    // ---- admission
+    while (next < order.size() && !free_slots.empty()) {
+      const int64_t c = order[next];
+      const int64_t n = job.offs[c + 1] - job.offs[c];
+      const size_t bytes = cell_bytes(n, eval_mem);
+      const size_t off = ctx.arena.alloc(bytes);
+      if (off == SIZE_MAX) break;
+      const int s = free_slots.back();
+      free_slots.pop_back();
+      Slot& sl = slots[s];
+      sl = Slot();
+      sl.cell = c;
+      sl.off = off;
+      sl.bytes = bytes;
+      OiCell& cd = hc[s];
+      std::memset(&cd, 0, sizeof(cd));
+      const int T = tiles_of(n);
+      const size_t nt = (size_t)T * (T + 1) / 2;
+      char* p = ctx.arena.ptr(off);
+      auto take = [&](size_t x) {
+        char* q = p;
+        p += (x + 255) & ~size_t(255);
+        return (double*)q;
+      };
+      cd.L = take(nt * OI_TILE * 8);
+      cd.W = eval_mem ? take(nt * OI_TILE * 8) : nullptr;
+      cd.Dinv = take((size_t)T * OI_TILE * 8);
+      cd.vec = take(4 * (size_t)T * OI_NB * 8);
+      cd.part = take((size_t)OI_PART_SIZE(nt, T) * 8);
+      cd.xyt = (const double*)d_xyt.p + 3 * job.offs[c];
+      cd.r = (const double*)d_r.p + job.offs[c];
+      cd.out = (double*)d_res.p + (size_t)s * OI_OUT_N;
+      cd.status = (int32_t*)d_stat.p + s;
+      cd.n = (int32_t)n;
+      cd.T = T;
+      if (job.xs) {
+        for (int d = 0; d < 3; ++d) cd.xs[d] = job.xs[3 * c + d];
+      }
+      cd.mean = job.mean;
+      if (job.kind == Job::FIT_PREDICT) {
+        sl.phase = 0;
+        oi::Vec x0;
+        for (int k = 0; k < oi::NH; ++k) x0[k] = job.x0[k];
+        sl.task = oi::cg_minimize(&sl.mail, x0, job.cg);
+        sl.task.start();  // runs to the first objective request
+      } else if (job.kind == Job::PREDICT_ONLY) {
+        sl.phase = 1;
+        for (int k = 0; k < 5; ++k) sl.hyp[k] = job.hyp[5 * c + k];
+      } else {
+        sl.phase = 2;
+        for (int k = 0; k < 5; ++k) sl.hyp[k] = std::exp(job.h[6 * c + k]);
+      }
+      active.push_back(s);
+      ++next;
+    }
+    if (active.empty()) return fail(OI_E_NOMEM, "workspace exhausted with no resident cell");
+
+    // ---- describe this round
+    std::vector<int> ev_slots, pr_slots;
+    for (int s : active) {
+      Slot& sl = slots[s];
+      OiCell& cd = hc[s];
+      if (sl.phase == 0) {
+        for (int k = 0; k < 5; ++k) cd.hyp[k] = std::exp(sl.mail.x[k]);  // GPR:120-122
+        cd.mode = OI_MODE_EVAL;
+        ev_slots.push_back(s);
+      } else if (sl.phase == 2) {
+        for (int k = 0; k < 5; ++k) cd.hyp[k] = sl.hyp[k];
+        cd.mode = OI_MODE_EVAL;
+        ev_slots.push_back(s);
+      } else {
+        for (int k = 0; k < 5; ++k) cd.hyp[k] = sl.hyp[k];
+        cd.mode = OI_MODE_PREDICT;
+        pr_slots.push_back(s);
+      }
+    }
+    auto byT = [&](std::vector<int>& v) {
+      std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return hc[a].T > hc[b].T; });
+    };
+    byT(ev_slots);
+    byT(pr_slots);
+    std::vector<int> all_slots;
+    all_slots.reserve(active.size());
+    std::merge(ev_slots.begin(), ev_slots.end(), pr_slots.begin(), pr_slots.end(),
+               std::back_inserter(all_slots), [&](int a, int b) { return hc[a].T > hc[b].T; });
+    const int na = (int)all_slots.size(), ne = (int)ev_slots.size(), np_ = (int)pr_slots.size();
+    int32_t* l_all = hl;
+    int32_t* l_ev = hl + cap;
+    int32_t* l_pr = hl + 2 * cap;
+    for (int k = 0; k < na; ++k) l_all[k] = all_slots[k];
+    for (int k = 0; k < ne; ++k) l_ev[k] = ev_slots[k];
+    for (int k = 0; k < np_; ++k) l_pr[k] = pr_slots[k];
+    const int maxT = na ? hc[all_slots[0]].T : 0;
+    const int maxTe = ne ? hc[ev_slots[0]].T : 0;
+
+    HIPC(hipMemcpyAsync(d_cells.p, hc, cap * sizeof(OiCell), hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_list.p, hl, cap * 4 * 3, hipMemcpyHostToDevice, st));
+    HIPC(hipMemsetAsync(d_stat.p, 0, cap * 4, st));
+    const int32_t* dl_all = dl;
+    const int32_t* dl_ev = dl + cap;
+    const int32_t* dl_pr = dl + 2 * cap;
+
+    // executed tile-GEMM flops per kernel (profile only)
+    const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
+    ev_kind.clear();
+    auto mark = [&](int k, bool end) {
+      if (!o.profile) return;
+      if (!end) ev_kind.push_back(k);
+      const size_t idx = 2 * (ev_kind.size() - 1) + (end ? 1 : 0);
+      if (idx < ev.size()) HIPC(hipEventRecord(ev[idx], st));
+    };
+    // ---- launch sequence
+    int rc = 0;
+    mark(K_BUILD, false);
+    rc |= oi_launch_build(dc, dl_all, na, maxT, st);
+    mark(K_BUILD, true);
+    for (int j = 0; j < maxT; ++j) {
+      int cnt = 0;
+      while (cnt < na && hc[all_slots[cnt]].T > j) ++cnt;
+      mark(K_CHOL, false);
+      rc |= oi_launch_chol_update(dc, dl_all, cnt, maxT, j, st);
+      mark(K_CHOL, true);
+      mark(K_TRSM, false);
+      rc |= oi_launch_trsm_trtri(dc, dl_all, cnt, maxT, j, st);
+      mark(K_TRSM, true);
+      if (o.profile) {
+        for (int k = 0; k < cnt; ++k) {
+          const OiCell& cd = hc[all_slots[k]];
+          kfl[K_CHOL] += tf * (double)(cd.T - j) * j;
+          kfl[K_TRSM] += tf * (double)(cd.T - 1 - j);
+          if (cd.mode == OI_MODE_EVAL)
+            for (int jj = 0; jj < j; ++jj) kfl[K_TRSM] += tf * (double)(j - jj + 1);
+        }
+      }
+    }
+    mark(K_ZVEC, false);
+    rc |= oi_launch_zvec(dc, dl_ev, ne, maxTe, st);
+    mark(K_ZVEC, true);
+    mark(K_AVEC, false);
+    rc |= oi_launch_avec(dc, dl_ev, ne, maxTe, st);
+    mark(K_AVEC, true);
+    mark(K_LAUUM, false);
+    rc |= oi_launch_lauum_grad(dc, dl_ev, ne, maxTe, st);
+    mark(K_LAUUM, true);
+    mark(K_FINAL, false);
+    rc |= oi_launch_finalize(dc, dl_ev, ne, st);
+    mark(K_FINAL, true);
+    mark(K_PRED, false);
+    rc |= oi_launch_predict(dc, dl_pr, np_, st);
+    mark(K_PRED, true);
+    if (rc) throw HipError(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    HIPC(hipMemcpyAsync(h_res.p, d_res.p, cap * OI_OUT_N * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h_stat.p, d_stat.p, cap * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    ++rounds;
+    if (o.profile) {
+      for (size_t q = 0; q < ev_kind.size() && 2 * q + 1 < ev.size(); ++q) {
+        float a = 0;
+        HIPC(hipEventElapsedTime(&a, ev[2 * q], ev[2 * q + 1]));
+        kms[ev_kind[q]] += a;
+        kln[ev_kind[q]]++;
+      }
+      for (int k = 0; k < ne; ++k) {
+        const OiCell& cd = hc[ev_slots[k]];
+        for (int i = 0; i < cd.T; ++i) kfl[K_LAUUM] += tf * (double)(cd.T - i) * (i + 1);
+      }
+    }
+
+    // ---- consume results
+    std::vector<int> still;
+    still.reserve(active.size());
+    for (int s : active) {
+      Slot& sl = slots[s];
+      const double* rr = hres + (size_t)s * OI_OUT_N;
+      const int64_t c = sl.cell;
+      bool done = false;
+      if (sl.phase == 0) {
+        ++evals;
+        sl.mail.f = rr[0];
+        for (int k = 0; k < oi::NH; ++k) sl.mail.g[k] = rr[1 + k];
+        sl.mail.pending = false;
+        sl.mail.waiter.resume();
+        if (sl.task.done()) {
+          sl.res = sl.task.result();
+          sl.phase = 1;
+          for (int k = 0; k < 5; ++k) sl.hyp[k] = std::exp(sl.res.x[k]);  // GPR:166-168
+        }
+      } else if (sl.phase == 2) {
+        ++evals;
+        job.nlz[c] = rr[0];
+        for (int k = 0; k < oi::NH; ++k) job.grad[6 * c + k] = rr[1 + k];
+        if (job.status) job.status[c] = hst[s];
+        done = true;
+      } else {
+        ++predicts;
+        double* dst = job.out + 8 * c;
+        dst[0] = rr[0];
+        dst[1] = rr[1];
+        dst[2] = rr[2];
+        for (int k = 0; k < 5; ++k) dst[3 + k] = sl.hyp[k];
+        if (hst[s] != OI_OK) {
+          for (int k = 0; k < 8; ++k) dst[k] = NAN;  // GPR:187-189
+        }
+        if (job.status) job.status[c] = hst[s];
+        if (job.info) {
+          int32_t* inf = job.info + 4 * c;
+          inf[0] = sl.res.nit;
+          inf[1] = sl.res.status;
+          inf[2] = (int32_t)sl.res.nfev;
+          inf[3] = (int32_t)sl.res.nobj;
+        }
+        done = true;
+      }
+      if (done) {
+        ctx.arena.release(sl.off, sl.bytes);
+        sl.task = oi::Task<oi::CgResult>();
+        sl.cell = -1;
+        free_slots.push_back(s);
+      } else {
+        still.push_back(s);
+      }
+    }
+    active.swap(still);
+  }
+  if (o.profile) {
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    std::lock_guard<std::mutex> pl(g_prof_mu);
+    for (int k = 0; k < K_COUNT; ++k) {
+      g_prof[k].launches += kln[k];
+      g_prof[k].ms += kms[k];
+      g_prof[k].flops += kfl[k];
+    }
+  }
+  {
+    std::lock_guard<std::mutex> pl(g_prof_mu);
+    g_run.rounds += rounds;
+    g_run.evals += evals;
+    g_run.predicts += predicts;
+    g_run.wall_s +=
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+  }
+  return 0;
+}
+
+bool check_offs(const int64_t* offs, int64_t ncell) {
+  if (!offs || offs[0] != 0) return false;
+  for (int64_t c = 0; c < ncell; ++c)
+    if (offs[c + 1] < offs[c]) return false;
+  return true;
+}
+
+int guarded(const Job& job, const oi_options* opts) {
+  oi_options o;
+  oi_options_default(&o);
+  if (opts) o = *opts;
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+      return fail(OI_E_NODEV, "no HIP device available");
+    if (o.device < 0 || o.device >= ndev) return fail(OI_E_ARG, "bad device ordinal");
+    return run(job, o);
+  } catch (const HipError& e) {
+    return fail(OI_E_HIP, e.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(OI_E_NOMEM, "host allocation failed");
+  }
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+void oi_options_default(oi_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->device = 0;
+  o->maxiter = -1;
+  o->gtol = 1e-5;
+  o->stream = nullptr;
+  o->pool_bytes = 0;
+  o->max_pool = 0;
+  o->profile = 0;
+}
+
+int oi_gpr_batch(const double* xyt, const double* z, const int64_t* offs, int64_t ncell,
+                 const double* xs, double mean, const double* x0, int32_t opt, const double* hyp,
+                 double* out, int32_t* status, int32_t* info, const oi_options* opts) {
+  if (ncell < 0 || !check_offs(offs, ncell)) return fail(OI_E_ARG, "bad offs / ncell");
+  if (ncell == 0) return 0;
+  const int64_t N = offs[ncell];
+  if ((N > 0 && (!xyt || !z)) || !xs || !out) return fail(OI_E_ARG, "null input/output pointer");
+  if (opt && !x0) return fail(OI_E_ARG, "opt=1 needs x0");
+  if (!opt && !hyp) return fail(OI_E_ARG, "opt=0 needs hyp");
+  Job job;
+  job.xyt = xyt;
+  job.offs = offs;
+  job.ncell = ncell;
+  job.r.resize(N);
+  // outputs - mX with mX = ones(n)*mean  (GPR:163, GPR:178)
+  const double m1 = 1.0 * mean;
+  for (int64_t a = 0; a < N; ++a) job.r[a] = z[a] - m1;
+  job.xs = xs;
+  job.mean = mean;
+  job.kind = opt ? Job::FIT_PREDICT : Job::PREDICT_ONLY;
+  job.x0 = x0;
+  job.hyp = hyp;
+  oi_options o;
+  oi_options_default(&o);
+  if (opts) o = *opts;
+  job.cg.gtol = o.gtol;
+  job.cg.maxiter = o.maxiter;
+  job.out = out;
+  job.status = status;
+  job.info = info;
+  return guarded(job, &o);
+}
+
+int oi_nlml_grad_batch(const double* xyt, const double* y, const double* mX, const int64_t* offs,
+                       int64_t ncell, const double* h, double* nlz, double* grad, int32_t* status,
+                       const oi_options* opts) {
+  if (ncell < 0 || !check_offs(offs, ncell)) return fail(OI_E_ARG, "bad offs / ncell");
+  if (ncell == 0) return 0;
+  const int64_t N = offs[ncell];
+  if ((N > 0 && (!xyt || !y || !mX)) || !h || !nlz || !grad)
+    return fail(OI_E_ARG, "null input/output pointer");
+  Job job;
+  job.xyt = xyt;
+  job.offs = offs;
+  job.ncell = ncell;
+  job.r.resize(N);
+  for (int64_t a = 0; a < N; ++a) job.r[a] = y[a] - mX[a];  // GPR:127
+  job.kind = Job::EVAL_ONLY;
+  job.h = h;
+  job.nlz = nlz;
+  job.grad = grad;
+  job.status = status;
+  return guarded(job, opts);
+}
+
+// ---- optimiser handle
+struct oi_cg {
+  oi::EvalSlot mail;
+  oi::Task<oi::CgResult> task;
+  bool started = false;
+};
+
+oi_cg* oi_cg_create(const double* x0, double gtol, int32_t maxiter) {
+  if (!x0) {
+    fail(OI_E_ARG, "null x0");
+    return nullptr;
+  }
+  auto* h = new oi_cg();
+  oi::Vec v;
+  for (int k = 0; k < oi::NH; ++k) v[k] = x0[k];
+  oi::CgOptions o;
+  o.gtol = gtol;
+  o.maxiter = maxiter;
+  h->task = oi::cg_minimize(&h->mail, v, o);
+  return h;
+}
+
+int oi_cg_step(oi_cg* h, double* x_req) {
+  if (!h) return fail(OI_E_ARG, "null handle");
+  if (!h->started) {
+    h->started = true;
+    h->task.start();
+  }
+  if (h->task.done()) return 0;
+  if (!h->mail.pending) return fail(OI_E_ARG, "oi_cg_step: optimiser in an invalid state");
+  if (x_req)
+    for (int k = 0; k < oi::NH; ++k) x_req[k] = h->mail.x[k];
+  return 1;
+}
+
+int oi_cg_feed(oi_cg* h, double f, const double* g) {
+  if (!h || !g) return fail(OI_E_ARG, "null argument");
+  if (!h->mail.pending) return fail(OI_E_ARG, "oi_cg_feed: no pending request");
+  h->mail.f = f;
+  for (int k = 0; k < oi::NH; ++k) h->mail.g[k] = g[k];
+  h->mail.pending = false;
+  h->mail.waiter.resume();
+  return 0;
+}
+
+int oi_cg_result(oi_cg* h, double* x, double* fun, int32_t* nit, int32_t* status, int64_t* nfev,
+                 int64_t* njev, int64_t* nobj) {
+  if (!h || !h->task.done()) return fail(OI_E_ARG, "optimiser not finished");
+  const oi::CgResult& r = h->task.result();
+  if (x)
+    for (int k = 0; k < oi::NH; ++k) x[k] = r.x[k];
+  if (fun) *fun = r.fun;
+  if (nit) *nit = r.nit;
+  if (status) *status = r.status;
+  if (nfev) *nfev = r.nfev;
+  if (njev) *njev = r.njev;
+  if (nobj) *nobj = r.nobj;
+  return 0;
+}
+
+void oi_cg_destroy(oi_cg* h) { delete h; }
+
+const char* oi_last_error(void) { return g_last_error.c_str(); }
+int32_t oi_version(void) { return OI_VERSION; }
+
+int64_t oi_profile_json(char* buf, int64_t len) {
+  std::lock_guard<std::mutex> pl(g_prof_mu);
+  std::string s = "{\"kernels\":{";
+  for (int k = 0; k < K_COUNT; ++k) {
+    char tmp[256];
+    std::snprintf(tmp, sizeof(tmp), "%s\"%s\":{\"launches\":%lld,\"total_ms\":%.6f,\"flops\":%.6e}",
+                  k ? "," : "", kKernelName[k], (long long)g_prof[k].launches, g_prof[k].ms,
+                  g_prof[k].flops);
+    s += tmp;
+  }
+  char tmp[256];
+  std::snprintf(tmp, sizeof(tmp), "},\"rounds\":%lld,\"evals\":%lld,\"predicts\":%lld,\"wall_s\":%.6f}",
+                (long long)g_run.rounds, (long long)g_run.evals, (long long)g_run.predicts,
+                g_run.wall_s);
+  s += tmp;
+  if (buf && len > 0) {
+    std::strncpy(buf, s.c_str(), (size_t)len);
+    buf[len - 1] = 0;
+  }
+  return (int64_t)s.size() + 1;
+}
+
+void oi_profile_reset(void) {
+  std::lock_guard<std::mutex> pl(g_prof_mu);
+  for (auto& k : g_prof) k = KStat();
+  g_run = RunStat();
+}
+
+}  // extern "C"

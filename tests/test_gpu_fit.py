@@ -1,0 +1,65 @@
+"""T3: end-to-end GPR3D(opt=True) on the GPU vs the oracle.
+
+scipy's CG stops on line-search failure in most cells, and its stopping point
+is chaotic in floating-point noise (re-running the reference on permuted
+observations moves fs by >1e-8 in ~23% of cells).  So per cell we require the
+GPU fit to be as good as the reference's -- nlZ(h_gpu) <= nlZ(h_ref) +
+1e-8 |nlZ(h_ref)| -- or its outputs to agree to 1e-6; and for the fleet a
+median fs rel-err <= 1e-8 and mean objective evaluations within 15%.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden, ragged_cell
+from oracle import gp_oracle as O
+from optimalinterpolation_amd import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def nlz_at(hyp5, x, y, mean):
+    h = np.r_[np.log(hyp5), np.log(.1)]
+    f, _ = O.neg_log_ml(h, x, y, np.ones(len(y)) * mean)
+    return float(np.asarray(f).item()) if np.ndim(f) else float(f)
+
+
+def check_fleet(xyt, z, offs, xs, mean, min_frac_good=0.999):
+    out, status, info = _lib.gpr_batch(xyt, z, offs, xs, mean, x0=np.array(O.X0_PRODUCTION),
+                                       opt=True, info=True)
+    rel, good, ev_gpu, ev_ref = [], 0, [], []
+    ncell = len(offs) - 1
+    for c in range(ncell):
+        a, b = offs[c], offs[c + 1]
+        x, y = xyt[a:b], z[a:b]
+        tr = []
+        ref = O.gp_cell(x, y, xs[c], mean, opt=True, trace=tr)
+        ev_ref.append(len(tr))
+        ev_gpu.append(info[c, 3])
+        r8 = np.array(ref, float)
+        rel.append(abs(out[c, 0] - r8[0]) / abs(r8[0]))
+        if np.allclose(out[c], r8, rtol=1e-6, atol=0, equal_nan=True):
+            good += 1
+            continue
+        if len(y) == 0:
+            continue
+        f_gpu = nlz_at(out[c, 3:8], x, y, mean)
+        f_ref = nlz_at(r8[3:8], x, y, mean)
+        if f_gpu <= f_ref + 1e-8 * abs(f_ref) + 1e-9:
+            good += 1
+    rel = np.array(rel)
+    assert good >= min_frac_good * ncell, (good, ncell)
+    assert np.median(rel) <= 1e-8, np.median(rel)
+    assert abs(np.mean(ev_gpu) / np.mean(ev_ref) - 1) <= 0.15, (np.mean(ev_gpu), np.mean(ev_ref))
+    return out, info
+
+
+def test_golden_gpr3d_fits():
+    d = load_golden('gpr3d.npz')
+    check_fleet(d['x'], d['y'], d['offs'], d['xs'], float(d['mean']))
+
+
+def test_synthetic_fleet_fits():
+    rng = np.random.default_rng(77)
+    sizes = rng.integers(20, 260, 40)
+    cells = synthetic.make_cells(sizes, seed=78)
+    check_fleet(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean)

@@ -1,0 +1,159 @@
+"""GPU parity of the HIP path (through the C ABI) against the oracle and the
+reference-generated golden fixtures.
+
+Tolerances (tier T1 -- fixed hyper-parameters):
+  nlZ, fs, sd, lZ     |gpu - ref| <= 1e-10 * max(1, |ref|)
+  gradient            |gpu - ref| <= 1e-10 * (|ref| + S_j),  S_j = 1/2 sum|Q o dK_j|
+                      (the magnitude of the terms the reference sums)
+Optimised fits (tier T3) are checked in tests/test_gpu_fit.py.
+"""
+import numpy as np
+import pytest
+from scipy.spatial.distance import pdist, squareform
+
+from conftest import load_golden, ragged_cell
+from oracle import gp_oracle as O
+from optimalinterpolation_amd import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-10
+
+
+def grad_scale(h, x, y, mX):
+    """S_j = 1/2 sum |Q o dK_j| (and sn2*sum|diag Q| for j=4) at h (oracle-side)."""
+    n = len(y)
+    if n == 0:
+        return np.zeros(6)
+    ell = np.exp(h[:3])
+    sf2, sn2 = np.exp(h[3]), np.exp(h[4])
+    K, dK = O.matern32(x, ell, sf2, grad=True)
+    Kinv = np.linalg.inv(K + np.eye(n) * sn2)
+    a = Kinv @ (y - mX)
+    Q = Kinv - np.outer(a, a)
+    s = np.zeros(6)
+    for j in range(3):
+        s[j] = np.abs(Q * dK[j]).sum() / 2
+    s[3] = np.abs(Q * 2 * K).sum() / 2
+    s[4] = sn2 * np.abs(np.diag(Q)).sum()
+    return s
+
+
+def close(a, b, scale=None, rtol=RTOL):
+    a = np.asarray(a, float)
+    b = np.asarray(b, float)
+    if scale is None:
+        scale = np.maximum(1.0, np.abs(b))
+    both_inf = np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b))
+    both_nan = np.isnan(a) & np.isnan(b)
+    ok = both_inf | both_nan | (np.abs(a - b) <= rtol * scale)
+    return bool(np.all(ok)), np.max(np.where(both_inf | both_nan, 0, np.abs(a - b) / scale))
+
+
+def test_smlii_golden():
+    d = load_golden('smlii.npz')
+    nc = len(d['nlZ'])
+    mX = np.full(len(d['y']), float(d['mean']))
+    nlz, grad, status = _lib.nlml_grad_batch(d['x'], d['y'], mX, d['offs'], d['h'])
+    for k in range(nc):
+        ok, err = close(nlz[k], d['nlZ'][k])
+        assert ok, (k, nlz[k], d['nlZ'][k], err)
+        x, y = ragged_cell(d, k)
+        if np.isfinite(d['nlZ'][k]):
+            sc = np.abs(d['g'][k]) + grad_scale(d['h'][k], x, y, np.ones(len(y)) * float(d['mean']))
+            ok, err = close(grad[k], d['g'][k], scale=np.maximum(sc, 1e-300))
+            assert ok, (k, grad[k], d['g'][k], err)
+
+
+@pytest.mark.parametrize('n', [63, 64, 65, 130, 333, 700, 1100])
+def test_smlii_vs_oracle_sizes(n):
+    """Tile-boundary sizes and multi-tile cells, 3 hyper points each."""
+    rng = np.random.default_rng(n)
+    cells = synthetic.make_cells([n] * 3, seed=n)
+    hs = np.array([O.X0_PRODUCTION,
+                   [np.log(3e5), np.log(2e5), np.log(8.), np.log(4e-3), np.log(5e-4), 0.0],
+                   [np.log(9e4), np.log(1.5e5), np.log(3.), np.log(1e-2), np.log(2e-3), -2.0]])
+    mX = np.full(len(cells.z), cells.mean)
+    nlz, grad, status = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, hs)
+    for c in range(3):
+        x, y, _ = cells.cell(c)
+        mx = np.ones(len(y)) * cells.mean
+        f, g = O.neg_log_ml(hs[c], x, y, mx)
+        f = float(np.asarray(f).item())
+        ok, err = close(nlz[c], f)
+        assert ok, (n, c, nlz[c], f, err)
+        sc = np.abs(g) + grad_scale(hs[c], x, y, mx)
+        ok, err = close(grad[c], g, scale=np.maximum(sc, 1e-300))
+        assert ok, (n, c, grad[c], g, err)
+    del rng
+
+
+def test_not_pd_reports_inf():
+    """Exactly duplicated sites with sn2 = 0 give a zero pivot: the reference's
+    LinAlgError branch (GPR:139-140) -> (inf, inf*ones)."""
+    x = np.array([[1e5, 2e5, 3.0], [1e5, 2e5, 3.0]])
+    y = np.array([0.3, 0.31])
+    h = np.array([[np.log(25000), np.log(25000), 0.0, 0.0, -np.inf, 0.0]])
+    f_ref, g_ref = O.neg_log_ml(h[0], x, y, np.ones(2) * 0.28)
+    assert np.isinf(f_ref)
+    nlz, grad, status = _lib.nlml_grad_batch(x, y, np.ones(2) * 0.28, np.array([0, 2]), h)
+    assert np.isinf(nlz[0]) and np.all(np.isinf(grad[0])) and status[0] == 1
+
+
+def test_predict_golden_gpr3d_pass2():
+    d = load_golden('gpr3d.npz')
+    out, status, _ = _lib.gpr_batch(d['x'], d['y'], d['offs'], d['xs'], float(d['mean']),
+                                    opt=False, hyp=d['hyp2'])
+    for c in range(len(d['offs']) - 1):
+        ok, err = close(out[c, :2], d['out2'][c])
+        assert ok, (c, out[c, :2], d['out2'][c], err)
+
+
+def test_predict_golden_64cells():
+    d = load_golden('predict64.npz')
+    out, status, _ = _lib.gpr_batch(d['x'], d['y'], d['offs'], d['xs'], float(d['mean']),
+                                    opt=False, hyp=d['hyp'])
+    ok, err = close(out[:, :2], d['out2'])
+    assert ok, err
+    assert np.all(status == 0)
+
+
+def test_predict_lZ_vs_oracle():
+    cells = synthetic.make_cells([0, 1, 5, 64, 200, 513], seed=5)
+    hyp = np.tile(synthetic.FIXED_HYPERS, (cells.ncell, 1))
+    out, status, _ = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean,
+                                    opt=False, hyp=hyp)
+    for c in range(cells.ncell):
+        x, y, xs = cells.cell(c)
+        fs, sd, lZ = O.predict(x, y, xs, cells.mean, hyp[c, :3], hyp[c, 3], hyp[c, 4])
+        ok, err = close(out[c, :3], [fs[0], sd[0], lZ])
+        assert ok, (c, out[c, :3], (fs[0], sd[0], lZ), err)
+    # n = 0: (mean, sqrt(sf2), -0.0) exactly like GPR:178-182 on empty arrays
+    assert out[0, 0] == cells.mean and out[0, 1] == np.sqrt(hyp[0, 3])
+    assert out[0, 2] == 0.0 and np.signbit(out[0, 2])
+
+
+def test_batch_composition_independence():
+    """A cell's results are bitwise identical alone or inside any batch."""
+    cells = synthetic.make_cells([150, 700, 40, 300], seed=9)
+    hs = np.tile(np.array([np.log(2e5), np.log(2e5), np.log(5.), np.log(5e-3), np.log(1e-3), 0.]),
+                 (4, 1))
+    mX = np.full(len(cells.z), cells.mean)
+    nlz, grad, _ = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, hs)
+    for c in range(4):
+        sub = cells.subset([c])
+        n1, g1, _ = _lib.nlml_grad_batch(sub.xyt, sub.z, np.full(len(sub.z), cells.mean), sub.offs,
+                                         hs[c:c + 1])
+        assert n1[0] == nlz[c] and np.array_equal(g1[0], grad[c])
+
+
+def test_gpr3d_n0_edge():
+    """GPR3D on an empty neighbourhood: CG stops at x0 and the
+    cell returns (mean, 1.0, -0.0, 25000, 25000, 1, 1, 1)."""
+    cells = synthetic.make_cells([0], seed=1)
+    out, status, info = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean,
+                                       x0=np.array(O.X0_PRODUCTION), opt=True, info=True)
+    ref = O.gp_cell(np.zeros((0, 3)), np.zeros(0), cells.xs[0], cells.mean, opt=True)
+    assert np.array_equal(out[0], np.array(ref, float))
+    assert np.signbit(out[0, 2])
+    assert info[0, 1] == 0 and info[0, 3] == 1
