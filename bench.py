@@ -1,0 +1,252 @@
+"""Benchmark: grid-cells/s for the full per-cell GP fit + predict (GPR3D,
+opt=True) on the synthetic 25 km pan-Arctic day, fp64 (BASELINE.json).
+
+A *step* is one shard of the day: the ~1e4 cells of the day (n ~ U{300..3000}
+observations each) are dealt by a seeded shuffle into
+8 shards of equal size; step s on rank r processes shard (s*N + r) mod 8.  So
+`--gpus 8 --steps 1` is exactly one whole day sharded over 8 GPUs (config 4)
+with the final RCCL gather of the posterior fields to rank 0, and
+`--gpus 1 --steps 2` times a quarter of the day on one GPU.
+
+Inputs are resident in HBM before the timed region (device-input C-ABI path);
+the timed region is bracketed by barrier + device synchronise on every rank,
+and the max over ranks is reported.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload day|predict|single]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 matrix (= vector) dense peak, spec
+NSHARDS = 8
+METRIC = "grid-cells/sec (full GP fit+predict), 25 km pan-Arctic day, fp64"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=2)
+    p.add_argument('--warmup', type=int, default=1)
+    p.add_argument('--workload', default='day', choices=['day', 'predict', 'single'])
+    p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--cpu-cores', type=int, default=0, help='0: min(16, affinity)')
+    p.add_argument('--out', default='')
+    return p.parse_args()
+
+
+# ----------------------------------------------------------------- workloads
+def build_steps(args, rank, world):
+    from optimalinterpolation_amd import synthetic
+    if args.workload == 'day':
+        day = synthetic.make_day(seed=args.seed)
+        perm = np.random.default_rng(args.seed + 99).permutation(day.ncell)
+        shards = [np.sort(perm[s::NSHARDS]) for s in range(NSHARDS)]
+        steps = []
+        for g in range(args.warmup + args.steps):
+            steps.append(day.subset(shards[(g * world + rank) % NSHARDS]))
+        cfg = {"workload": "25km pan-Arctic day (config 3/4): opt=True fit+predict per cell",
+               "day_cells": int(day.ncell), "n_obs_per_cell": "U{300..3000}",
+               "grid_km": 25, "cells_per_step": int(len(shards[0])), "shards": NSHARDS,
+               "x0": "GPR_CS2S3.py:217", "parallelism": f"dp{world} (cells sharded, RCCL gather)"}
+        return steps, True, cfg
+    if args.workload == 'predict':
+        cells = synthetic.make_cells([500] * 1000, seed=args.seed + rank)
+        cfg = {"workload": "config 2: 1000 cells x n=500, fixed hypers (predict-only)",
+               "cells_per_step": 1000, "parallelism": f"dp{world}"}
+        return [cells] * (args.warmup + args.steps), False, cfg
+    cells = synthetic.make_cells([200], seed=args.seed + rank)
+    cfg = {"workload": "config 1: single cell, n=200, opt=True", "cells_per_step": 1,
+           "parallelism": f"dp{world}"}
+    return [cells] * (args.warmup + args.steps), True, cfg
+
+
+# ----------------------------------------------------------------- cpu baseline
+CPU_PROBE = r'''
+import os, sys, time, json
+os.environ["OPENBLAS_NUM_THREADS"] = "1"; os.environ["OMP_NUM_THREADS"] = "1"
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from oracle import gp_oracle as O
+from optimalinterpolation_amd import synthetic
+n = int(sys.argv[2]); reps = int(sys.argv[3])
+cells = synthetic.make_cells([n], seed=n)
+x, y, xs = cells.cell(0)
+mX = np.ones(n) * cells.mean
+h = np.array([np.log(3e5), np.log(3e5), np.log(10.), np.log(5e-3), np.log(1e-3), np.log(.1)])
+te = []
+for _ in range(reps):
+    t = time.perf_counter(); O.neg_log_ml(h, x, y, mX); te.append(time.perf_counter() - t)
+tp = []
+for _ in range(reps):
+    t = time.perf_counter(); O.predict(x, y, xs, cells.mean, np.exp(h[:3]), np.exp(h[3]), np.exp(h[4])); tp.append(time.perf_counter() - t)
+print(json.dumps({"n": n, "eval_s": min(te), "pred_s": min(tp)}))
+'''
+
+
+def cpu_baseline(sizes, evals, cores):
+    """Time the CPU oracle (a bit-exact NumPy/SciPy restatement of the
+    reference, oracle/gp_oracle.py) per objective evaluation and per predict
+    at probe sizes, one process per core with single-threaded OpenBLAS (like
+    the reference's one MPI rank per core); fit t(n) = a + b n^3 and
+    extrapolate over the timed cells with their measured evaluation counts."""
+    probes = [(300, 5), (600, 3), (1000, 2), (1500, 1), (2000, 1), (2500, 1), (3000, 1)]
+    t0 = time.time()
+    procs = []
+    res = []
+    for i in range(0, len(probes), cores):
+        procs = [subprocess.Popen([sys.executable, '-c', CPU_PROBE, ROOT, str(n), str(r)],
+                                  stdout=subprocess.PIPE, text=True) for n, r in probes[i:i + cores]]
+        for p in procs:
+            out, _ = p.communicate(timeout=600)
+            res.append(json.loads(out.strip().splitlines()[-1]))
+    wall = time.time() - t0
+    ns = np.array([r['n'] for r in res], float)
+    A = np.stack([np.ones_like(ns), ns ** 3], 1)
+    ce, *_ = np.linalg.lstsq(A, np.array([r['eval_s'] for r in res]), rcond=None)
+    cp, *_ = np.linalg.lstsq(A, np.array([r['pred_s'] for r in res]), rcond=None)
+    n = np.asarray(sizes, float)
+    t_cells = evals * (ce[0] + ce[1] * n ** 3) + (cp[0] + cp[1] * n ** 3)
+    core_s = float(np.sum(t_cells))
+    value = len(sizes) / (core_s / cores)
+    return {"value": value, "unit": "grid-cells/s", "cores": cores, "kind": "port",
+            "sample": (f"oracle/gp_oracle.py (bit-exact restatement of GPR_CS2S3.py:78-191, scipy CG) "
+                       f"timed per SMLII eval and per predict at n={[int(p[0]) for p in probes]} "
+                       f"({wall:.0f} s wall, 1 OpenBLAS thread per process), fitted t=a+b*n^3, "
+                       f"extrapolated over the {len(sizes)} timed cells x their measured evals/cell "
+                       f"({float(np.mean(evals)):.1f} mean) on {cores} cores: extrapolated"),
+            "probe": res}
+
+
+# ----------------------------------------------------------------- main
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group('nccl')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    from optimalinterpolation_amd import _lib
+
+    steps, opt, cfg = build_steps(args, rank, world)
+    x0 = np.array([np.log(25e3), np.log(25e3), 0.0, 0.0, 0.0, np.log(.1)])
+    hyp = None
+    from optimalinterpolation_amd import synthetic
+    # inputs resident in HBM before timing
+    dev_steps = []
+    for cells in steps:
+        xyt = torch.from_numpy(cells.xyt).to(dev).contiguous()
+        z = torch.from_numpy(cells.z).to(dev).contiguous()
+        h = None if opt else np.tile(synthetic.FIXED_HYPERS, (cells.ncell, 1))
+        dev_steps.append((cells, xyt, z, h))
+    torch.cuda.synchronize()
+
+    def run_step(k, profile):
+        cells, xyt, z, h = dev_steps[k]
+        return _lib.gpr_batch_device(xyt, z, cells.offs, cells.xs, cells.mean, x0=x0 if opt else None,
+                                     opt=opt, hyp=h, info=True, device=local, profile=profile)
+
+    for k in range(args.warmup):
+        run_step(k, False)
+    _lib.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = []
+    for k in range(args.warmup, args.warmup + args.steps):
+        outs.append(run_step(k, True))
+    # the single gather of posterior fields (ncell x 8 fp64) to rank 0 over RCCL
+    res = torch.from_numpy(np.concatenate([o[0] for o in outs])).to(dev)
+    if world > 1:
+        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([res.shape[0]], device=dev))
+        mx = int(max(s.item() for s in sizes))
+        padded = torch.zeros((mx, 8), dtype=torch.float64, device=dev)
+        padded[:res.shape[0]] = res
+        bufs = [torch.zeros_like(padded) for _ in range(world)] if rank == 0 else None
+        dist.gather(padded, bufs, dst=0)
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ncells_rank = sum(steps[k].ncell for k in range(args.warmup, args.warmup + args.steps))
+    tot = torch.tensor([float(ncells_rank)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    total_cells = float(tot.item())
+
+    prof = _lib.profile_json()
+    info = np.concatenate([o[2] for o in outs])
+    sizes_timed = np.concatenate([np.diff(steps[k].offs) for k in range(args.warmup, args.warmup + args.steps)])
+    evals = info[:, 3].astype(float) if opt else np.zeros(len(sizes_timed))
+    # useful (algorithmic) flops, SURVEY §8d: F = E (n^3 + 40 n^2) + n^3/3 + 16 n^2 per cell
+    n = sizes_timed.astype(float)
+    useful = float(np.sum(evals * (n ** 3 + 40 * n ** 2) + n ** 3 / 3 + 16 * n ** 2))
+    kern = prof['kernels']
+    gemm = {k: v for k, v in kern.items() if v['flops'] > 0 and v['total_ms'] > 0}
+    dom = max(gemm, key=lambda k: gemm[k]['total_ms']) if gemm else max(kern, key=lambda k: kern[k]['total_ms'])
+    kd = kern[dom]
+    achieved = kd['flops'] / (kd['total_ms'] / 1e3) / 1e12 if kd['total_ms'] > 0 else 0.0
+    traffic = None
+    tfile = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get(dom, {}).get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+    roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
+                "launches": kd['launches'], "avg_launch_ms": kd['total_ms'] / max(kd['launches'], 1),
+                "flops_per_launch": kd['flops'] / max(kd['launches'], 1),
+                "flop_model": "executed fp64 MFMA tile products, 2*64^3 each (padded tiles)",
+                "kernels_ms": {k: round(v['total_ms'], 3) for k, v in kern.items()},
+                "useful_tflops_per_gpu": round(useful / dt / 1e12, 3),
+                "useful_frac_per_gpu": round(useful / dt / 1e12 / PEAK_FP64_TFLOPS, 4),
+                "useful_flop_model": "SURVEY §8d: E*(n^3+40n^2) + n^3/3 + 16n^2 per cell, unpadded n"}
+
+    line = {"metric": METRIC if args.workload == 'day' else f"grid-cells/sec ({args.workload}), fp64",
+            "value": round(total_cells / dt, 4), "unit": "grid-cells/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded SURVEY §8d generator; reference data not shipped)",
+            "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
+            "roofline": roofline}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        try:
+            line["cpu_baseline"] = cpu_baseline(sizes_timed, evals, cores)
+        except Exception as e:  # never lose the GPU line over the baseline
+            line["cpu_baseline"] = {"value": None, "error": repr(e)}
+    else:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, 'w') as f:
+                f.write(s + '\n')
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -46,6 +46,8 @@ typedef struct oi_options {
   int64_t pool_bytes;  /* device workspace budget; 0 => 60% of free HBM */
   int32_t max_pool;    /* max cells resident at once; 0 => automatic */
   int32_t profile;     /* 1 => record per-kernel HIP-event timings (oi_profile_json) */
+  int32_t device_inputs; /* 1 => xyt / z / y / mX are DEVICE pointers already resident
+                            in HBM on `device` (offs, xs, x0, hyp, h stay on the host) */
 } oi_options;
 
 /* Fill *o with defaults. */

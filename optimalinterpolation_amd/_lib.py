@@ -38,7 +38,8 @@ EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_cr
 class OiOptions(ctypes.Structure):
     _fields_ = [('device', ctypes.c_int32), ('maxiter', ctypes.c_int32), ('gtol', ctypes.c_double),
                 ('stream', ctypes.c_void_p), ('pool_bytes', ctypes.c_int64),
-                ('max_pool', ctypes.c_int32), ('profile', ctypes.c_int32)]
+                ('max_pool', ctypes.c_int32), ('profile', ctypes.c_int32),
+                ('device_inputs', ctypes.c_int32)]
 
 
 class OiError(RuntimeError):
@@ -96,7 +97,8 @@ def _check(rc):
         raise OiError(f"liboi error {rc}: {load().oi_last_error().decode(errors='replace')}")
 
 
-def options(device=0, maxiter=-1, gtol=1e-5, stream=None, pool_bytes=0, max_pool=0, profile=False):
+def options(device=0, maxiter=-1, gtol=1e-5, stream=None, pool_bytes=0, max_pool=0, profile=False,
+            device_inputs=False):
     o = OiOptions()
     load().oi_options_default(ctypes.byref(o))
     o.device = int(device)
@@ -106,6 +108,7 @@ def options(device=0, maxiter=-1, gtol=1e-5, stream=None, pool_bytes=0, max_pool
     o.pool_bytes = int(pool_bytes)
     o.max_pool = int(max_pool)
     o.profile = 1 if profile else 0
+    o.device_inputs = 1 if device_inputs else 0
     return o
 
 
@@ -130,6 +133,36 @@ def gpr_batch(xyt, z, offs, xs, mean, x0=None, opt=True, hyp=None, info=False, *
         raise ValueError("opt=False needs hyp [ncell x 5]")
     o = options(**opt_kw)
     rc = lib.oi_gpr_batch(_ptr(xyt, ctypes.c_double), _ptr(z, ctypes.c_double),
+                          _ptr(offs, ctypes.c_int64), ncell, _ptr(xs, ctypes.c_double),
+                          float(mean), _ptr(x0a, ctypes.c_double), 1 if opt else 0,
+                          _ptr(hypa, ctypes.c_double), _ptr(out, ctypes.c_double),
+                          _ptr(status, ctypes.c_int32), _ptr(inf, ctypes.c_int32), ctypes.byref(o))
+    _check(rc)
+    return out, status, inf
+
+
+def gpr_batch_device(xyt_dev, z_dev, offs, xs, mean, x0=None, opt=True, hyp=None, info=False,
+                     **opt_kw):
+    """oi_gpr_batch with inputs already resident in HBM: ``xyt_dev`` / ``z_dev``
+    are device tensors (anything with ``data_ptr()``, fp64, contiguous) on
+    ``opt_kw['device']``; the metadata stays on the host."""
+    lib = load()
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1, 3)
+    ncell = len(offs) - 1
+    N = int(offs[-1])
+    if xs.shape[0] != ncell or offs[0] != 0 or z_dev.numel() != N or xyt_dev.numel() != 3 * N:
+        raise ValueError("inconsistent ragged batch")
+    if not (xyt_dev.is_contiguous() and z_dev.is_contiguous()):
+        raise ValueError("device inputs must be contiguous")
+    out = np.empty((ncell, 8))
+    status = np.zeros(ncell, dtype=np.int32)
+    inf = np.zeros((ncell, 4), dtype=np.int32) if info else None
+    x0a = np.ascontiguousarray(x0, dtype=np.float64) if x0 is not None else None
+    hypa = np.ascontiguousarray(hyp, dtype=np.float64).reshape(-1, 5) if hyp is not None else None
+    o = options(device_inputs=True, **opt_kw)
+    rc = lib.oi_gpr_batch(ctypes.cast(xyt_dev.data_ptr(), c_double_p),
+                          ctypes.cast(z_dev.data_ptr(), c_double_p),
                           _ptr(offs, ctypes.c_int64), ncell, _ptr(xs, ctypes.c_double),
                           float(mean), _ptr(x0a, ctypes.c_double), 1 if opt else 0,
                           _ptr(hypa, ctypes.c_double), _ptr(out, ctypes.c_double),

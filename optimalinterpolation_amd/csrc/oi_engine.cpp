@@ -200,11 +200,12 @@ struct HBuf {  // pinned host
 
 // ------------------------------------------------------------- the batch
 struct Job {
-  // inputs (host)
+  // inputs (host, or device when opts.device_inputs)
   const double* xyt;
   const int64_t* offs;
   int64_t ncell;
-  std::vector<double> r;        // y - mX
+  const double* y = nullptr;    // observations
+  const double* mX = nullptr;   // per-observation prior mean, or null => `mean`
   const double* xs = nullptr;   // ncell x 3 (predict)
   double mean = 0.0;
   // per-cell work description
@@ -240,13 +241,23 @@ int run(const Job& job, const oi_options& o) {
   const int64_t ncell = job.ncell;
   const int64_t N = job.offs[ncell];
 
-  // inputs to device once
-  DBuf d_xyt, d_r;
-  d_xyt.reserve(std::max<size_t>(N * 3 * 8, 256));
+  // inputs to device once; residuals r = y - mX (GPR:127, GPR:178)
+  DBuf d_xyt_own, d_r, d_y_own, d_m_own;
+  const double* d_xyt = job.xyt;
   d_r.reserve(std::max<size_t>(N * 8, 256));
-  if (N > 0) {
-    HIPC(hipMemcpyAsync(d_xyt.p, job.xyt, N * 3 * 8, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(d_r.p, job.r.data(), N * 8, hipMemcpyHostToDevice, st));
+  if (!o.device_inputs) {
+    d_xyt_own.reserve(std::max<size_t>(N * 3 * 8, 256));
+    d_xyt = (const double*)d_xyt_own.p;
+    if (N > 0) {
+      std::vector<double> r(N);
+      for (int64_t a = 0; a < N; ++a) r[a] = job.y[a] - (job.mX ? job.mX[a] : 1.0 * job.mean);
+      HIPC(hipMemcpyAsync(d_xyt_own.p, job.xyt, N * 3 * 8, hipMemcpyHostToDevice, st));
+      HIPC(hipMemcpyAsync(d_r.p, r.data(), N * 8, hipMemcpyHostToDevice, st));
+      HIPC(hipStreamSynchronize(st));  // r is a local host buffer
+    }
+  } else if (N > 0) {
+    if (oi_launch_residual(job.y, job.mX, job.mean, (double*)d_r.p, N, st))
+      throw HipError("residual kernel launch failed");
   }
   const bool eval_mem = job.kind != Job::PREDICT_ONLY;
 
@@ -328,7 +339,7 @@ int run(const Job& job, const oi_options& o) {
       cd.Dinv = take((size_t)T * OI_TILE * 8);
       cd.vec = take(4 * (size_t)T * OI_NB * 8);
       cd.part = take((size_t)OI_PART_SIZE(nt, T) * 8);
-      cd.xyt = (const double*)d_xyt.p + 3 * job.offs[c];
+      cd.xyt = d_xyt + 3 * job.offs[c];
       cd.r = (const double*)d_r.p + job.offs[c];
       cd.out = (double*)d_res.p + (size_t)s * OI_OUT_N;
       cd.status = (int32_t*)d_stat.p + s;
@@ -582,6 +593,7 @@ void oi_options_default(oi_options* o) {
   o->pool_bytes = 0;
   o->max_pool = 0;
   o->profile = 0;
+  o->device_inputs = 0;
 }
 
 int oi_gpr_batch(const double* xyt, const double* z, const int64_t* offs, int64_t ncell,
@@ -597,10 +609,8 @@ int oi_gpr_batch(const double* xyt, const double* z, const int64_t* offs, int64_
   job.xyt = xyt;
   job.offs = offs;
   job.ncell = ncell;
-  job.r.resize(N);
-  // outputs - mX with mX = ones(n)*mean  (GPR:163, GPR:178)
-  const double m1 = 1.0 * mean;
-  for (int64_t a = 0; a < N; ++a) job.r[a] = z[a] - m1;
+  job.y = z;  // outputs - mX with mX = ones(n)*mean  (GPR:163, GPR:178)
+  job.mX = nullptr;
   job.xs = xs;
   job.mean = mean;
   job.kind = opt ? Job::FIT_PREDICT : Job::PREDICT_ONLY;
@@ -629,8 +639,8 @@ int oi_nlml_grad_batch(const double* xyt, const double* y, const double* mX, con
   job.xyt = xyt;
   job.offs = offs;
   job.ncell = ncell;
-  job.r.resize(N);
-  for (int64_t a = 0; a < N; ++a) job.r[a] = y[a] - mX[a];  // GPR:127
+  job.y = y;
+  job.mX = mX;  // y - mX, GPR:127
   job.kind = Job::EVAL_ONLY;
   job.h = h;
   job.nlz = nlz;

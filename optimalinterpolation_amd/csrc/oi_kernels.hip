@@ -632,6 +632,13 @@ __global__ __launch_bounds__(256) void k_predict(const OiCell* __restrict__ cell
   }
 }
 
+// ---------------------------------------------------------- k_residual
+__global__ void k_residual(const double* __restrict__ y, const double* __restrict__ mX,
+                           double mean, double* __restrict__ r, int64_t N) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a < N) r[a] = y[a] - (mX ? mX[a] : 1.0 * mean);
+}
+
 // ------------------------------------------------------------ launchers
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 static inline int ret() { return hipGetLastError() == hipSuccess ? 0 : -1; }
@@ -711,5 +718,13 @@ extern "C" int oi_launch_finalize(const OiCell* cells, const int32_t* list, int 
                                   void* stream) {
   if (ncell <= 0) return 0;
   hipLaunchKernelGGL(k_finalize, dim3(ncell), dim3(256), 0, S(stream), cells, list);
+  return ret();
+}
+
+extern "C" int oi_launch_residual(const double* y, const double* mX, double mean, double* r,
+                                  int64_t N, void* stream) {
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(k_residual, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, S(stream), y, mX,
+                     mean, r, N);
   return ret();
 }
