@@ -1,0 +1,74 @@
+"""Multi-rank sharding + gather with the gloo backend on CPU,
+world_size 2 and 3.  The compute step is a CPU stand-in (the oracle's predict)
+so the test exercises partitioning, the collective and the re-ordering; the
+GPU compute step is the same driver with driver.gpu_compute()."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from optimalinterpolation_amd import driver, synthetic
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def oracle_compute(sub):
+    from oracle import gp_oracle as O
+    out = np.zeros((sub.ncell, 8))
+    for c in range(sub.ncell):
+        x, y, xs = sub.cell(c)
+        h = synthetic.FIXED_HYPERS
+        fs, sd, lZ = O.predict(x, y, xs, sub.mean, h[:3], h[3], h[4])
+        out[c] = [fs[0], sd[0], lZ, *h]
+    return out, np.zeros(sub.ncell, np.int32), np.zeros((sub.ncell, 4), np.int32)
+
+
+def _worker(rank, world, port, partition, q):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    cells = synthetic.make_cells([0, 3, 17, 40, 9, 64, 65, 1, 30], seed=21)
+    full = driver.run_sharded(cells, oracle_compute, rank, world, partition=partition)
+    if rank == 0:
+        q.put(full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,partition', [(2, 'lpt'), (3, 'strided')])
+def test_sharded_equals_single_rank(world, partition):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, partition, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    cells = synthetic.make_cells([0, 3, 17, 40, 9, 64, 65, 1, 30], seed=21)
+    ref, _, _ = oracle_compute(cells)
+    assert full.shape == (cells.ncell, 13)
+    assert np.array_equal(full[:, :8], ref)
+
+
+def test_partitions_cover_every_cell_once():
+    sizes = np.random.default_rng(0).integers(300, 3001, 1000)
+    for world in (1, 2, 5, 8):
+        for parts in (driver.lpt_partition(driver.cell_costs(sizes), world),
+                      driver.strided_partition(len(sizes), world)):
+            allc = np.sort(np.concatenate(parts))
+            assert np.array_equal(allc, np.arange(len(sizes)))
+    parts = driver.lpt_partition(driver.cell_costs(sizes), 8)
+    loads = [driver.cell_costs(sizes)[p].sum() for p in parts]
+    assert max(loads) / min(loads) < 1.01
