@@ -26,6 +26,7 @@ struct OiCell {
   double* L;          // packed lower tiles (T(T+1)/2 * 4096)
   double* W;          // packed lower tiles of L^-1 (eval mode), else null
   double* Dinv;       // T * 4096
+  double* P;          // T * 4096: P_jk = -Dinv_jj L_jk of the current block column
   double* vec;        // 4 * T * 64: z | alpha | kstar | v
   double* part;       // partial sums, see OI_PART_*
   const double* xyt;  // n x 3 inputs (device)
@@ -36,7 +37,7 @@ struct OiCell {
   double hyp[5];      // lx, ly, lt, sf2, sn2 (the values the objective uses)
   double xs[3];       // prediction target (predict mode)
   double mean;        // prior mean (predict mode)
-  double pad2_[3];
+  double pad2_[2];
 };
 
 // partial-sum layout inside OiCell::part (ntile = T(T+1)/2)
@@ -56,10 +57,10 @@ extern "C" {
 // kernel launchers (oi_kernels.hip); `cells` and `list` are device pointers,
 // `list` holds indices into `cells` sorted by T descending.
 int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
-int oi_launch_chol_update(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                          void* stream);
-int oi_launch_trsm_trtri(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                         void* stream);
+int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
+int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
+int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
+                         int with_trtri, void* stream);
 int oi_launch_zvec(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,

@@ -109,15 +109,16 @@ size_t cell_bytes(int64_t n, bool eval) {
   add(nt * OI_TILE * 8);                         // L
   if (eval) add(nt * OI_TILE * 8);               // W
   add(T * OI_TILE * 8);                          // Dinv
+  add(T * OI_TILE * 8);                          // P
   add(4 * T * OI_NB * 8);                        // vec
   add((size_t)OI_PART_SIZE(nt, T) * 8);          // part
   return b;
 }
 
 // ------------------------------------------------------------- profiling
-enum KernelId { K_BUILD, K_CHOL, K_TRSM, K_ZVEC, K_AVEC, K_LAUUM, K_FINAL, K_PRED, K_COUNT };
-const char* kKernelName[K_COUNT] = {"k_build",  "k_chol_update", "k_trsm_trtri", "k_zvec",
-                                    "k_avec",   "k_lauum_grad",  "k_finalize",   "k_predict"};
+enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_ZVEC, K_AVEC, K_LAUUM, K_FINAL, K_PRED, K_COUNT };
+const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_chol_panel", "k_zvec",
+                                    "k_avec",  "k_lauum_grad",  "k_finalize", "k_predict"};
 struct KStat {
   int64_t launches = 0;
   double ms = 0.0;
@@ -129,6 +130,17 @@ struct RunStat {
   int64_t rounds = 0, evals = 0, predicts = 0;
   double wall_s = 0.0;
 } g_run;
+struct LaunchRec {
+  int kind, j, cells;
+  double ms;
+};
+std::vector<LaunchRec> g_last_round;  // per-launch times of the latest profiled round
+struct RoundRec {
+  int n_eval, n_pred, maxT;
+  double work;  // sum over evaluated cells of T^3
+  double ms;    // GPU time of the round's launches
+};
+std::vector<RoundRec> g_rounds;  // every profiled round since the last reset
 
 // ------------------------------------------------------------- context
 struct Context {
@@ -337,6 +349,7 @@ int run(const Job& job, const oi_options& o) {
       cd.L = take(nt * OI_TILE * 8);
       cd.W = eval_mem ? take(nt * OI_TILE * 8) : nullptr;
       cd.Dinv = take((size_t)T * OI_TILE * 8);
+      cd.P = take((size_t)T * OI_TILE * 8);
       cd.vec = take(4 * (size_t)T * OI_NB * 8);
       cd.part = take((size_t)OI_PART_SIZE(nt, T) * 8);
       cd.xyt = d_xyt + 3 * job.offs[c];
@@ -415,36 +428,50 @@ int run(const Job& job, const oi_options& o) {
     // executed tile-GEMM flops per kernel (profile only)
     const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
     ev_kind.clear();
+    std::vector<std::pair<int, int>> ev_meta;  // (j, cells) per launch
+    int cur_j = -1, cur_cells = 0;
     auto mark = [&](int k, bool end) {
       if (!o.profile) return;
-      if (!end) ev_kind.push_back(k);
+      if (!end) {
+        ev_kind.push_back(k);
+        ev_meta.emplace_back(cur_j, cur_cells);
+      }
       const size_t idx = 2 * (ev_kind.size() - 1) + (end ? 1 : 0);
       if (idx < ev.size()) HIPC(hipEventRecord(ev[idx], st));
     };
     // ---- launch sequence
     int rc = 0;
+    cur_cells = na;
     mark(K_BUILD, false);
     rc |= oi_launch_build(dc, dl_all, na, maxT, st);
     mark(K_BUILD, true);
     for (int j = 0; j < maxT; ++j) {
       int cnt = 0;
       while (cnt < na && hc[all_slots[cnt]].T > j) ++cnt;
+      cur_j = j;
+      cur_cells = cnt;
       mark(K_CHOL, false);
-      rc |= oi_launch_chol_update(dc, dl_all, cnt, maxT, j, st);
+      rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, st);
       mark(K_CHOL, true);
+      mark(K_SCALE, false);
+      rc |= oi_launch_scale(dc, dl_all, cnt, j, st);
+      mark(K_SCALE, true);
       mark(K_TRSM, false);
-      rc |= oi_launch_trsm_trtri(dc, dl_all, cnt, maxT, j, st);
+      rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, st);
       mark(K_TRSM, true);
-      if (o.profile) {
+      if (o.profile) {  // executed MFMA flops: each workgroup = 64 x 128 products
         for (int k = 0; k < cnt; ++k) {
           const OiCell& cd = hc[all_slots[k]];
-          kfl[K_CHOL] += tf * (double)(cd.T - j) * j;
-          kfl[K_TRSM] += tf * (double)(cd.T - 1 - j);
+          kfl[K_SCALE] += tf * (double)j;
+          kfl[K_TRSM] += tf * (double)(cd.T - 1 - j) * (j + 1);
+          if (cd.T - 1 - j > 0) kfl[K_TRSM] += tf * (double)(j + 1);  // look-ahead diagonal
           if (cd.mode == OI_MODE_EVAL)
-            for (int jj = 0; jj < j; ++jj) kfl[K_TRSM] += tf * (double)(j - jj + 1);
+            for (int jj = 0; jj < j; ++jj) kfl[K_TRSM] += tf * (double)(j - jj);
         }
       }
     }
+    cur_j = -1;
+    cur_cells = ne;
     mark(K_ZVEC, false);
     rc |= oi_launch_zvec(dc, dl_ev, ne, maxTe, st);
     mark(K_ZVEC, true);
@@ -466,15 +493,25 @@ int run(const Job& job, const oi_options& o) {
     HIPC(hipStreamSynchronize(st));
     ++rounds;
     if (o.profile) {
+      std::vector<LaunchRec> recs;
       for (size_t q = 0; q < ev_kind.size() && 2 * q + 1 < ev.size(); ++q) {
         float a = 0;
         HIPC(hipEventElapsedTime(&a, ev[2 * q], ev[2 * q + 1]));
         kms[ev_kind[q]] += a;
         kln[ev_kind[q]]++;
+        recs.push_back({ev_kind[q], ev_meta[q].first, ev_meta[q].second, (double)a});
+      }
+      double rms = 0.0, work = 0.0;
+      for (const auto& rr : recs) rms += rr.ms;
+      for (int k = 0; k < ne; ++k) work += std::pow((double)hc[ev_slots[k]].T, 3.0);
+      {
+        std::lock_guard<std::mutex> pl(g_prof_mu);
+        g_last_round.swap(recs);
+        g_rounds.push_back({ne, np_, maxT, work, rms});
       }
       for (int k = 0; k < ne; ++k) {
         const OiCell& cd = hc[ev_slots[k]];
-        for (int i = 0; i < cd.T; ++i) kfl[K_LAUUM] += tf * (double)(cd.T - i) * (i + 1);
+        for (int i = 0; i < cd.T; ++i) kfl[K_LAUUM] += 2 * tf * (double)(cd.T - i) * (i / 2 + 1);
       }
     }
 
@@ -725,10 +762,25 @@ int64_t oi_profile_json(char* buf, int64_t len) {
     s += tmp;
   }
   char tmp[256];
-  std::snprintf(tmp, sizeof(tmp), "},\"rounds\":%lld,\"evals\":%lld,\"predicts\":%lld,\"wall_s\":%.6f}",
+  std::snprintf(tmp, sizeof(tmp), "},\"rounds\":%lld,\"evals\":%lld,\"predicts\":%lld,\"wall_s\":%.6f",
                 (long long)g_run.rounds, (long long)g_run.evals, (long long)g_run.predicts,
                 g_run.wall_s);
   s += tmp;
+  s += ",\"last_round\":[";
+  for (size_t q = 0; q < g_last_round.size(); ++q) {
+    const LaunchRec& r = g_last_round[q];
+    std::snprintf(tmp, sizeof(tmp), "%s[\"%s\",%d,%d,%.4f]", q ? "," : "", kKernelName[r.kind], r.j,
+                  r.cells, r.ms);
+    s += tmp;
+  }
+  s += "],\"rounds_log\":[";
+  for (size_t q = 0; q < g_rounds.size(); ++q) {
+    const RoundRec& r = g_rounds[q];
+    std::snprintf(tmp, sizeof(tmp), "%s[%d,%d,%d,%.0f,%.4f]", q ? "," : "", r.n_eval, r.n_pred, r.maxT,
+                  r.work, r.ms);
+    s += tmp;
+  }
+  s += "]}";
   if (buf && len > 0) {
     std::strncpy(buf, s.c_str(), (size_t)len);
     buf[len - 1] = 0;
@@ -740,6 +792,7 @@ void oi_profile_reset(void) {
   std::lock_guard<std::mutex> pl(g_prof_mu);
   for (auto& k : g_prof) k = KStat();
   g_run = RunStat();
+  g_rounds.clear();
 }
 
 }  // extern "C"

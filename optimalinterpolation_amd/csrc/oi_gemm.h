@@ -1,0 +1,192 @@
+// fp64 MFMA tile-GEMM core shared by the kernels (oi_kernels.hip) and the
+// micro-benchmarks (tools/gemm_probe*.hip).
+//
+// A 512-thread workgroup (8 waves) computes a 64 x 128 block D = [D0 | D1]:
+//   D[m][n] += sum_p sum_k A_p[k*64 + m] * Bh_p[k*64 + n']     (n = 64h + n')
+// i.e. two 64x64 output tiles that share the A operand.  All operands are
+// "k-major" 64x64 tiles (a column-major tile X used as X[m][k], or a row-major
+// tile used as X^T), so global -> LDS staging is contiguous 16 B per lane.
+// Wave w owns rows 32*((w>>2)&1) .. +32 and columns 32*(w&3) .. +32 as 2x2
+// blocks of v_mfma_f64_16x16x4f64; lane l of block (mb, nb) holds
+//   D[32wr + 16mb + (l>>4) + 4r][32wc + 16nb + (l&15)],  r = 0..3.
+// Measured on MI355X (tools/gemm_probe2.hip, v7): 63 TF/s with both operands
+// streamed from HBM vs 48.5 TF/s for a 256-thread 64x64 tile.
+#pragma once
+#include <hip/hip_runtime.h>
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+#define GNB 64
+#define KC 16                          // k-depth of one staged chunk
+#define LDSA 80                        // A chunk row stride (doubles)
+#define LDSB 144                       // B chunk row stride: rows k, k+1 land in
+                                       // opposite bank halves for ds_read_b64
+#define STAGE_A (KC * LDSA)
+#define STAGE_B (KC * LDSB)
+#define GEMM2_LDS (2 * (STAGE_A + STAGE_B))  // 7168 doubles = 56 KiB
+#define GEMM_THREADS 512
+
+struct Quad {
+  d4 c[2][2];
+};
+
+__device__ __forceinline__ void quad_zero(Quad& q) {
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) q.c[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+}
+
+// coordinates in the 64 x 128 block of accumulator entry (mb, nb, r) of this lane
+__device__ __forceinline__ int acc_row(int mb, int r) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  return 32 * ((w >> 2) & 1) + 16 * mb + (lane >> 4) + 4 * r;
+}
+__device__ __forceinline__ int acc_col(int nb) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  return 32 * (w & 3) + 16 * nb + (lane & 15);
+}
+
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0)
+
+// pair(p, a, b0, b1): the p-th operand triple (A tile, B tile of the left
+// half, B tile of the right half).  Register staging, two LDS buffers.
+template <class PairFn>
+__device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = (w >> 2) & 1, wc = w & 3;
+  const int nch = npairs * (GNB / KC);
+  if (nch == 0) return;
+  const int tt = t & 255, half = t >> 8;
+  const int sk = tt >> 4, sm = (tt & 15) * 4;
+  double2 ra0, ra1, rb0, rb1;
+  auto load = [&](int ch) {
+    const double *pa, *pb0, *pb1;
+    pair(ch >> 2, pa, pb0, pb1);
+    const int off = (ch & 3) * KC * GNB + tt * 4;
+    if (half == 0) {
+      ra0 = *(const double2*)(pa + off);
+      ra1 = *(const double2*)(pa + off + 2);
+    }
+    const double* pb = half ? pb1 : pb0;
+    rb0 = *(const double2*)(pb + off);
+    rb1 = *(const double2*)(pb + off + 2);
+  };
+  auto store = [&](int buf) {
+    double* As = lds + buf * (STAGE_A + STAGE_B);
+    double* Bs = As + STAGE_A;
+    if (half == 0) {
+      *(double2*)(As + sk * LDSA + sm) = ra0;
+      *(double2*)(As + sk * LDSA + sm + 2) = ra1;
+    }
+    *(double2*)(Bs + sk * LDSB + 64 * half + sm) = rb0;
+    *(double2*)(Bs + sk * LDSB + 64 * half + sm + 2) = rb1;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int ch = 0; ch < nch; ++ch) {
+    if (ch + 1 < nch) load(ch + 1);
+    const double* As = lds + (ch & 1) * (STAGE_A + STAGE_B);
+    const double* Bs = As + STAGE_A;
+#pragma unroll
+    for (int kk = 0; kk < KC / 4; ++kk) {
+      const int k = kk * 4 + fk;
+      const double a0 = As[k * LDSA + 32 * wr + fr];
+      const double a1 = As[k * LDSA + 32 * wr + 16 + fr];
+      const double b0 = Bs[k * LDSB + 32 * wc + fr];
+      const double b1 = Bs[k * LDSB + 32 * wc + 16 + fr];
+      acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+      acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+      acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+      acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+    }
+    if (ch + 1 < nch) store((ch + 1) & 1);
+    __syncthreads();
+  }
+}
+
+// D2 = Dj * S for a 64 x 128 S held in LDS as [k][n] (row stride LDSB), with
+// Dj a column-major 64x64 tile read straight from global memory as the A
+// operand (it is shared by all of a cell's workgroups: L2-resident).
+__device__ __forceinline__ void times_tile(Quad& acc2, const double* __restrict__ Dj,
+                                           const double* Ss) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = (w >> 2) & 1, wc = w & 3;
+  const int fr = lane & 15, fk = lane >> 4;
+  quad_zero(acc2);
+#pragma unroll 4
+  for (int kk = 0; kk < GNB / 4; ++kk) {
+    const int k = kk * 4 + fk;
+    const double a0 = Dj[k * GNB + 32 * wr + fr];
+    const double a1 = Dj[k * GNB + 32 * wr + 16 + fr];
+    const double b0 = Ss[k * LDSB + 32 * wc + fr];
+    const double b1 = Ss[k * LDSB + 32 * wc + 16 + fr];
+    acc2.c[0][0] = MFMA64(a0, b0, acc2.c[0][0]);
+    acc2.c[0][1] = MFMA64(a0, b1, acc2.c[0][1]);
+    acc2.c[1][0] = MFMA64(a1, b0, acc2.c[1][0]);
+    acc2.c[1][1] = MFMA64(a1, b1, acc2.c[1][1]);
+  }
+}
+
+// ---- 256-thread variant: one 64x64 output tile, wave w owns the 32x32
+// quadrant (32*(w>>1), 32*(w&1)); LDS 2 x (A, B) chunks of 16 x 80 = 40 KiB,
+// so four workgroups fit a CU.
+#define GEMM1_LDS (4 * STAGE_A)
+__device__ __forceinline__ int acc1_row(int mb, int r) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  return 32 * (w >> 1) + 16 * mb + (lane >> 4) + 4 * r;
+}
+__device__ __forceinline__ int acc1_col(int nb) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  return 32 * (w & 1) + 16 * nb + (lane & 15);
+}
+
+template <class PairFn>
+__device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int nch = npairs * (GNB / KC);
+  if (nch == 0) return;
+  const int sk = t >> 4, sm = (t & 15) * 4;
+  double2 ra0, ra1, rb0, rb1;
+  auto load = [&](int ch) {
+    const double *pa, *pb;
+    pair(ch >> 2, pa, pb);
+    const int off = (ch & 3) * KC * GNB + t * 4;
+    ra0 = *(const double2*)(pa + off);
+    ra1 = *(const double2*)(pa + off + 2);
+    rb0 = *(const double2*)(pb + off);
+    rb1 = *(const double2*)(pb + off + 2);
+  };
+  auto store = [&](int buf) {
+    double* As = lds + buf * 2 * STAGE_A;
+    double* Bs = As + STAGE_A;
+    *(double2*)(As + sk * LDSA + sm) = ra0;
+    *(double2*)(As + sk * LDSA + sm + 2) = ra1;
+    *(double2*)(Bs + sk * LDSA + sm) = rb0;
+    *(double2*)(Bs + sk * LDSA + sm + 2) = rb1;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int ch = 0; ch < nch; ++ch) {
+    if (ch + 1 < nch) load(ch + 1);
+    const double* As = lds + (ch & 1) * 2 * STAGE_A;
+    const double* Bs = As + STAGE_A;
+#pragma unroll
+    for (int kk = 0; kk < KC / 4; ++kk) {
+      const int k = kk * 4 + fk;
+      const double a0 = As[k * LDSA + 32 * wr + fr];
+      const double a1 = As[k * LDSA + 32 * wr + 16 + fr];
+      const double b0 = Bs[k * LDSA + 32 * wc + fr];
+      const double b1 = Bs[k * LDSA + 32 * wc + 16 + fr];
+      acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+      acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+      acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+      acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+    }
+    if (ch + 1 < nch) store((ch + 1) & 1);
+    __syncthreads();
+  }
+}

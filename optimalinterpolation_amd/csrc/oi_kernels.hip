@@ -3,17 +3,22 @@
 // for a ragged batch of independent grid cells.  Data layout: oi_device.h.
 //
 // Per objective evaluation of a cell (T = ceil(n/64) tiles per side):
-//   k_build        K + sn2 I (Matern-3/2, GPR:93-94)                    O(n^2)
-//   k_chol_update  left-looking Cholesky, block column j: tile GEMMs on
-//                  v_mfma_f64_16x16x4f64; the diagonal tile is then
-//                  factored and inverted in LDS                          n^3/3
-//   k_trsm_trtri   L_ij = A_ij L_jj^-T  and  row j of W = L^-1           n^3/3
-//   k_zvec/k_avec  z = W r, alpha = W^T z (K^-1 r, GPR:127)              O(n^2)
-//   k_lauum_grad   K^-1 = W^T W tile by tile, fused with the gradient
-//                  traces sum((K^-1 - alpha alpha^T) o dK_j) with K, dK_j
-//                  regenerated from coordinates (GPR:130-138)            n^3/3
+//   k_build        K + sn2 I (Matern-3/2, GPR:93-94)                         O(n^2)
+//   k_diag_factor(j) factor + invert diagonal tile j: one wave per cell, rows in
+//                  registers (potrf + trti2, fully unrolled)             ~n^2 * 64
+//   k_chol_panel(j)  left-looking Cholesky, block column j, two row tiles per
+//                  512-thread workgroup sharing the L_j. panel:
+//                  L_ij^T = Dinv_jj (A_ij - sum_{k<j} L_ik L_jk^T)^T  (update and
+//                  triangular solve fused), the workgroup of the first tile
+//                  pair then applies the GEMM update of diagonal tile j+1
+//                  (look-ahead); plus row j of W = L^-1:
+//                  W_j,jj = -Dinv_jj sum_{k=jj}^{j-1} L_jk W_k,jj         2 n^3/3
+//   k_zvec/k_avec  z = W r, alpha = W^T z  (alpha = K^-1 r, GPR:127)          O(n^2)
+//   k_lauum_grad   K^-1 = W^T W, two tiles per workgroup, fused with the
+//                  gradient traces sum((K^-1 - alpha alpha^T) o dK_j); K and
+//                  dK_j are regenerated from coordinates (GPR:130-138)         n^3/3
 //   k_finalize     nlZ and dnlZ (GPR:128, GPR:131-138), fixed-order sums
-// Predict (GPR:173-182): k_build, Cholesky, then k_predict (two triangular
+// Predict (GPR:173-182): k_build, the Cholesky, then k_predict (two triangular
 // solves per cell + fs / sd / lZ).
 //
 // Every reduction has a fixed order that depends only on the cell, so a
@@ -22,17 +27,15 @@
 #include <math.h>
 
 #include "oi_device.h"
-
-typedef double d4 __attribute__((ext_vector_type(4)));
+#include "oi_gemm.h"
 
 #define NB OI_NB
-#define LDSS 80                 // LDS row stride (doubles): rows k and k+1 fall in
-                                // opposite bank halves for ds_read_b64
-#define KC 16                   // k-depth of one staged chunk
-#define STAGE (KC * LDSS)       // doubles per staged operand chunk
-#define GEMM_LDS (4 * STAGE)    // [2 buffers][A, B] = 40 KiB
 #define SQRT3 1.7320508075688772
 #define LOG2PI 1.8378770664093453  // np.log(2*np.pi)
+
+// structurally-zero operand tile (tiles above the block diagonal); device
+// globals are zero-initialised by the loader and never written
+__device__ double g_zero_tile[OI_TILE];
 
 __device__ __forceinline__ size_t tri(int i) { return (size_t)i * (i + 1) / 2; }
 __device__ __forceinline__ double* tileL(const OiCell& c, int i, int j) {
@@ -45,87 +48,10 @@ __device__ __forceinline__ double* tileD(const OiCell& c, int j) {
   return c.Dinv + (size_t)j * OI_TILE;
 }
 
-// ------------------------------------------------------------------ GEMM
-// One 256-thread workgroup computes a 64x64 tile D. Wave w owns the 32x32
-// quadrant (32*(w>>1), 32*(w&1)) as 2x2 blocks of the 16x16 fp64 MFMA.
-// Lane l of block (mb, nb) holds D[16mb + (l>>4) + 4r][16nb + (l&15)], r=0..3.
-struct Quad {
-  d4 c[2][2];
-};
-
-__device__ __forceinline__ void quad_zero(Quad& q) {
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b) q.c[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
-}
-
-// element coordinates of accumulator entry (mb, nb, r) for this lane
-__device__ __forceinline__ int acc_row(int mb, int r) {
-  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  return 32 * (w >> 1) + 16 * mb + (lane >> 4) + 4 * r;
-}
-__device__ __forceinline__ int acc_col(int nb) {
-  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  return 32 * (w & 1) + 16 * nb + (lane & 15);
-}
-
-// D[m][n] += sum_p sum_k A_p[k*64 + m] * B_p[k*64 + n]
-// ("k-major" 64x64 operand tiles: a column-major tile X used as X[m][k], or a
-// row-major tile used as X^T).  `pair(p, a, b)` returns the p-th tile pair.
-// Staging: global -> registers -> LDS, double-buffered in KC-deep chunks.
-template <class PairFn>
-__device__ __forceinline__ void gemm_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wr = w >> 1, wc = w & 1;
-  const int nch = npairs * (NB / KC);
-  if (nch == 0) return;
-  // this thread stages 4 consecutive doubles (k = t/16, m = 4*(t%16)) per operand
-  const int sk = t >> 4, sm = (t & 15) * 4;
-  double2 ra0, ra1, rb0, rb1;
-  auto load = [&](int ch) {
-    const double *pa, *pb;
-    pair(ch >> 2, pa, pb);
-    const int off = (ch & 3) * KC * NB + t * 4;
-    ra0 = *(const double2*)(pa + off);
-    ra1 = *(const double2*)(pa + off + 2);
-    rb0 = *(const double2*)(pb + off);
-    rb1 = *(const double2*)(pb + off + 2);
-  };
-  auto store = [&](int buf) {
-    double* As = lds + buf * 2 * STAGE;
-    double* Bs = As + STAGE;
-    *(double2*)(As + sk * LDSS + sm) = ra0;
-    *(double2*)(As + sk * LDSS + sm + 2) = ra1;
-    *(double2*)(Bs + sk * LDSS + sm) = rb0;
-    *(double2*)(Bs + sk * LDSS + sm + 2) = rb1;
-  };
-  load(0);
-  store(0);
-  __syncthreads();
-  const int fr = lane & 15, fk = lane >> 4;
-  for (int ch = 0; ch < nch; ++ch) {
-    if (ch + 1 < nch) load(ch + 1);
-    const double* As = lds + (ch & 1) * 2 * STAGE;
-    const double* Bs = As + STAGE;
-#pragma unroll
-    for (int kk = 0; kk < KC / 4; ++kk) {
-      const int k = kk * 4 + fk;
-      double a0 = As[k * LDSS + 32 * wr + fr];
-      double a1 = As[k * LDSS + 32 * wr + 16 + fr];
-      double b0 = Bs[k * LDSS + 32 * wc + fr];
-      double b1 = Bs[k * LDSS + 32 * wc + 16 + fr];
-      acc.c[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc.c[0][0], 0, 0, 0);
-      acc.c[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc.c[0][1], 0, 0, 0);
-      acc.c[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc.c[1][0], 0, 0, 0);
-      acc.c[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc.c[1][1], 0, 0, 0);
-    }
-    if (ch + 1 < nch) store((ch + 1) & 1);
-    __syncthreads();
-  }
-}
-
-// deterministic block reduction of NV values (256 threads), result valid in thread 0
-template <int NV>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double* red /* >= 4*NV */) {
+// deterministic block reduction of NV values, result valid in thread 0;
+// red must hold NWAVES*NV doubles
+template <int NV, int NWAVES>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
   for (int q = 0; q < NV; ++q) {
@@ -138,7 +64,11 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red /* >= 4*N
     for (int q = 0; q < NV; ++q) red[w * NV + q] = v[q];
   __syncthreads();
   if (t == 0)
-    for (int q = 0; q < NV; ++q) v[q] = ((red[q] + red[NV + q]) + red[2 * NV + q]) + red[3 * NV + q];
+    for (int q = 0; q < NV; ++q) {
+      double s = red[q];
+      for (int ww = 1; ww < NWAVES; ++ww) s += red[ww * NV + q];
+      v[q] = s;
+    }
 }
 
 __device__ __forceinline__ bool decode_tri(int x, int T, int& i, int& j) {
@@ -151,13 +81,44 @@ __device__ __forceinline__ bool decode_tri(int x, int T, int& i, int& j) {
   return true;
 }
 
+// lauum work slots: block row i owns floor(i/2)+1 column pairs (2J, 2J+1);
+// slots before row i: S(2a) = a(a+1), S(2a+1) = (a+1)^2
+__device__ __host__ __forceinline__ int lauum_slots_before(int i) {
+  const int a = i >> 1;
+  return (i & 1) ? (a + 1) * (a + 1) : a * (a + 1);
+}
+__device__ __forceinline__ bool decode_pair(int x, int T, int& i, int& J) {
+  if (x >= lauum_slots_before(T)) return false;
+  int ii = (int)(2.0 * sqrt((double)x));
+  while (ii > 0 && lauum_slots_before(ii) > x) --ii;
+  while (lauum_slots_before(ii + 1) <= x) ++ii;
+  i = ii;
+  J = x - lauum_slots_before(ii);
+  return true;
+}
+
+// Blocks are dealt round-robin over the 8 XCDs (b, b+8, ... share one).  Deal
+// whole CELLS round-robin instead: block b works on cell (b&7) + 8*((b>>3)/gx),
+// slot (b>>3) % gx, so all tiles of a cell run on one XCD and share its L2,
+// while neighbouring cells (similar sizes: the list is sorted by T) spread
+// over all XCDs.  The grid is gx * roundup(ncell, 8) blocks.
+__device__ __forceinline__ bool xcd_cell_slot(int gx, int ncell, int& cell, int& x) {
+  const int b = blockIdx.x, t = b >> 3;
+  cell = (b & 7) + 8 * (t / gx);
+  x = t % gx;
+  return cell < ncell;
+}
+
 // ------------------------------------------------------------- k_build
 // K + sn2*I for tile (i, j), GPR:93-94 and GPR:126; identity on padding.
 __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
-                                               const int32_t* __restrict__ list) {
-  const OiCell& c = cells[list[blockIdx.y]];
+                                               const int32_t* __restrict__ list, int gx,
+                                               int ncell) {
+  int ci, x;
+  if (!xcd_cell_slot(gx, ncell, ci, x)) return;
+  const OiCell& c = cells[list[ci]];
   int i, j;
-  if (!decode_tri(blockIdx.x, c.T, i, j)) return;
+  if (!decode_tri(x, c.T, i, j)) return;
   __shared__ double u[2][3][NB];
   const int t = threadIdx.x, n = c.n;
   if (t < 2 * NB) {
@@ -182,196 +143,239 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
   }
 }
 
-// --------------------------------------------------- diagonal tile: potrf
-// In-place lower Cholesky of S (64x64, stride 65) with 256 threads.
-// Fails exactly when a pivot is <= 0 (NaN pivots propagate, as with the
-// reference's numpy/OpenBLAS cholesky).  Returns false on failure.
-__device__ bool potrf_lds(double* S) {
-  const int t = threadIdx.x;
+// --------------------------------------------- k_diag_factor(j)
+// Factor + invert diagonal tile j of every cell: one 64-lane wave per cell,
+// lane r holding row r of the tile in registers (fully unrolled loops, column
+// values broadcast with v_readlane).  The tile already holds the updated
+// A_jj - sum_{k<j} L_jk L_jk^T (k_chol_panel(j-1) wrote it; for j = 0 it is
+// K + sn2 I from k_build).  Writes L_jj, its log-determinant, Dinv_jj and
+// (eval mode) W_jj.  Pivot <= 0 -> status = not PD (GPR:139-140); NaN pivots
+// propagate like the reference's numpy/OpenBLAS cholesky.
+__device__ __forceinline__ double rdlane(double v, int lane) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffLL), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+__global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ cells,
+                                                   const int32_t* __restrict__ list, int j) {
+  __shared__ double Tt[NB * 65];  // transpose buffer for the row-major W_jj
+  const OiCell& c = cells[list[blockIdx.x]];
+  if (j >= c.T || *c.status != OI_OK) return;
+  const int r = threadIdx.x;
+  double* Y = tileL(c, j, j);
+  double R[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) R[q] = Y[q * NB + r];  // row r of the column-major tile
+  // ---- potrf (right-looking): scale column cc by 1/sqrt(pivot), update the rest
+  bool ok = true;
+#pragma unroll
   for (int cc = 0; cc < NB; ++cc) {
-    __syncthreads();
-    const double d = S[cc * 65 + cc];
-    if (d <= 0.0) return false;  // uniform: every thread read the same value
+    const double d = rdlane(R[cc], cc);
+    ok = ok && !(d <= 0.0);
     const double l = sqrt(d);
-    __syncthreads();
-    if (t == 0) S[cc * 65 + cc] = l;
-    if (t > cc && t < NB) S[t * 65 + cc] /= l;
-    __syncthreads();
-    const int m = NB - 1 - cc;
-    for (int e = t; e < m * m; e += 256) {
-      int rr = e / m, ss = e - rr * m;
-      if (ss <= rr) {
-        int r = cc + 1 + rr, s = cc + 1 + ss;
-        S[r * 65 + s] -= S[r * 65 + cc] * S[s * 65 + cc];
-      }
-    }
+    const double lr = r > cc ? R[cc] / l : 0.0;
+    R[cc] = r > cc ? lr : (r == cc ? l : R[cc]);
+#pragma unroll
+    for (int s2 = cc + 1; s2 < NB; ++s2) R[s2] -= lr * rdlane(R[cc], s2);
   }
-  __syncthreads();
-  return true;
-}
-
-// In-place inverse of the lower-triangular S (LAPACK trti2 order: last column first).
-__device__ void trtri_lds(double* S, double* tmp) {
-  const int t = threadIdx.x;
+  if (!ok) {
+    if (r == 0) *c.status = OI_NOT_PD;
+    return;
+  }
+  double lg = 0.0;
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (q > r) R[q] = 0.0;                                   // clear the upper part
+    if (q == r) lg = (j * NB + r < c.n) ? log(R[q]) : 0.0;   // log L_rr
+    Y[q * NB + r] = R[q];                                    // L_jj, column-major
+  }
+  for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
+  if (r == 0) {
+    const int ntile = c.T * (c.T + 1) / 2;
+    c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
+  }
+  // ---- trti2, last column first: x = Inv[r][cc+1..r] . L[cc+1..r][cc],
+  //      column cc := -x / L[cc][cc]   (LAPACK dtrti2 order)
+#pragma unroll
   for (int cc = NB - 1; cc >= 0; --cc) {
-    __syncthreads();
-    const double ajj = 1.0 / S[cc * 65 + cc];
+    const double ajj = 1.0 / rdlane(R[cc], cc);
     double x = 0.0;
-    if (t > cc && t < NB) {
-      // x_t = sum_{k=cc+1}^{t} Sinv[t][k] * S[k][cc]
-      for (int k = cc + 1; k <= t; ++k) x += S[t * 65 + k] * S[k * 65 + cc];
-    }
-    __syncthreads();
-    if (t == 0) S[cc * 65 + cc] = ajj;
-    if (t > cc && t < NB) S[t * 65 + cc] = -ajj * x;
+#pragma unroll
+    for (int k = cc + 1; k < NB; ++k) x += R[k] * rdlane(R[cc], k);
+    R[cc] = r > cc ? -ajj * x : (r == cc ? ajj : R[cc]);
   }
-  __syncthreads();
-  (void)tmp;
+  double* Dj = tileD(c, j);
+#pragma unroll
+  for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
+  if (c.mode == OI_MODE_EVAL) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) Tt[q * 65 + r] = R[q];  // Tt[c][r] = Inv[r][c]
+    __syncthreads();
+    double* Wj = tileW(c, j, j);
+    for (int q = 0; q < NB; ++q) Wj[q * NB + r] = Tt[r * 65 + q];  // W[q][r], row-major
+  }
 }
 
-// ------------------------------------------------------- k_chol_update(j)
-// Tile (i, j), i >= j:  A_ij -= sum_{k<j} L_ik L_jk^T  (computed transposed so
-// that loads and stores of the column-major tiles are coalesced).  The
-// diagonal tile is then factored, inverted, and its log-determinant recorded.
-__global__ __launch_bounds__(256) void k_chol_update(const OiCell* __restrict__ cells,
-                                                     const int32_t* __restrict__ list, int j) {
-  __shared__ __attribute__((aligned(16))) double lds[GEMM_LDS];
-  const OiCell& c = cells[list[blockIdx.y]];
-  const int i = j + blockIdx.x;
-  if (i >= c.T || *c.status != OI_OK) return;
-  Quad acc;
-  quad_zero(acc);
-  gemm_kmajor(acc, lds, j, [&](int p, const double*& a, const double*& b) {
-    a = tileL(c, j, p);
-    b = tileL(c, i, p);
-  });
-  double* Y = tileL(c, i, j);
-  double val[2][2][4];
-  for (int mb = 0; mb < 2; ++mb)
-    for (int nb = 0; nb < 2; ++nb)
-      for (int r = 0; r < 4; ++r) {
-        int m = acc_row(mb, r), nn = acc_col(nb);
-        val[mb][nb][r] = Y[m * NB + nn] - acc.c[mb][nb][r];  // (Y^T)[m][nn]
-      }
-  if (i != j) {
+// ----------------------------------------------------------- k_scale(j)
+// P_jk = -Dinv_jj L_jk for k < j (column-major), so that the panel tiles and
+// the row of W become single GEMM loops (no separate Dinv product per tile).
+// A 256-thread workgroup handles SCALE_KPW tiles k of one cell: the Dinv_jj
+// operand stays in registers, each L_jk is staged transposed through LDS and
+// D = P^T = -L_jk^T Dinv_jj^T is stored coalesced as P[n][m].
+#define SCALE_KPW 4
+__global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
+                                               const int32_t* __restrict__ list, int j, int gx,
+                                               int ncell) {
+  __shared__ __attribute__((aligned(16))) double As[NB * LDSA];  // As[q][m] = L_jk[q][m]
+  int ci, g;
+  if (!xcd_cell_slot(gx, ncell, ci, g)) return;
+  const OiCell& c = cells[list[ci]];
+  const int k0 = g * SCALE_KPW;
+  if (j >= c.T || k0 >= j || *c.status != OI_OK) return;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const double* D = tileD(c, j);
+  double b0[NB / 4], b1[NB / 4];  // B[q][n] = Dinv[n][q] at q*64 + n
+#pragma unroll
+  for (int kk = 0; kk < NB / 4; ++kk) {
+    const int q = kk * 4 + fk;
+    b0[kk] = D[q * NB + 32 * wc + fr];
+    b1[kk] = D[q * NB + 32 * wc + 16 + fr];
+  }
+  const int sm = t >> 2, sq = (t & 3) * 16;  // staging: column sm, rows sq..sq+15
+  for (int k = k0; k < k0 + SCALE_KPW && k < j; ++k) {
+    const double* L = tileL(c, j, k);
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u += 2) {
+      const double2 x = *(const double2*)(L + sm * NB + sq + u);
+      v[u] = x.x;
+      v[u + 1] = x.y;
+    }
+    __syncthreads();  // previous tile's reads of As are done
+#pragma unroll
+    for (int u = 0; u < 16; ++u) As[(sq + u) * LDSA + sm] = v[u];
+    __syncthreads();
+    Quad acc;
+    quad_zero(acc);
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const int q = kk * 4 + fk;
+      const double a0 = As[q * LDSA + 32 * wr + fr], a1 = As[q * LDSA + 32 * wr + 16 + fr];
+      acc.c[0][0] = MFMA64(a0, b0[kk], acc.c[0][0]);
+      acc.c[0][1] = MFMA64(a0, b1[kk], acc.c[0][1]);
+      acc.c[1][0] = MFMA64(a1, b0[kk], acc.c[1][0]);
+      acc.c[1][1] = MFMA64(a1, b1[kk], acc.c[1][1]);
+    }
+    double* P = c.P + (size_t)k * OI_TILE;
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
-        for (int r = 0; r < 4; ++r) Y[acc_row(mb, r) * NB + acc_col(nb)] = val[mb][nb][r];
-    return;
-  }
-  // ---- diagonal tile: factor + invert in LDS
-  double* S = lds;  // 64 x 65
-  __shared__ double red[16];
-  __syncthreads();
-  for (int mb = 0; mb < 2; ++mb)
-    for (int nb = 0; nb < 2; ++nb)
-      for (int r = 0; r < 4; ++r) S[acc_row(mb, r) * 65 + acc_col(nb)] = val[mb][nb][r];
-  const bool ok = potrf_lds(S);
-  const int t = threadIdx.x;
-  if (!ok) {
-    if (t == 0) *c.status = OI_NOT_PD;
-    return;
-  }
-  // L_jj back to global (column-major, zero upper triangle)
-  for (int e = t; e < OI_TILE; e += 256) {
-    int r = e & 63, cc = e >> 6;
-    Y[e] = r >= cc ? S[r * 65 + cc] : 0.0;
-  }
-  // log-determinant contribution of this diagonal tile
-  {
-    double v[1] = {0.0};
-    if (t < NB && j * NB + t < c.n) v[0] = log(S[t * 65 + t]);
-    block_sum<1>(v, red);
-    if (t == 0) {
-      const int ntile = c.T * (c.T + 1) / 2;
-      c.part[OI_PART_LOGDET(ntile, c.T) + j] = v[0];
-    }
-  }
-  trtri_lds(S, nullptr);
-  double* Dj = tileD(c, j);
-  for (int e = t; e < OI_TILE; e += 256) {
-    int r = e & 63, cc = e >> 6;
-    Dj[e] = r >= cc ? S[r * 65 + cc] : 0.0;  // column-major
-  }
-  if (c.mode == OI_MODE_EVAL) {
-    double* Wj = tileW(c, j, j);
-    for (int e = t; e < OI_TILE; e += 256) {
-      int r = e >> 6, cc = e & 63;
-      Wj[e] = r >= cc ? S[r * 65 + cc] : 0.0;  // row-major
-    }
+        for (int r = 0; r < 4; ++r) {
+          const int m = 32 * wr + 16 * mb + (lane >> 4) + 4 * r, n = 32 * wc + 16 * nb + (lane & 15);
+          P[m * NB + n] = -acc.c[mb][nb][r];  // D[m][n] = (Dinv L)[n][m] -> P[n][m]
+        }
   }
 }
 
-// --------------------------------------------------- k_trsm_trtri(j)
-// blockIdx.x <  T-1-j : L_ij = A_ij Dinv_jj^T for i = j+1+x      (trsm)
-// blockIdx.x >= T-1-j : W_j,jj = -Dinv_jj sum_{k=jj}^{j-1} L_jk W_k,jj (row j of L^-1)
-__global__ __launch_bounds__(256) void k_trsm_trtri(const OiCell* __restrict__ cells,
-                                                    const int32_t* __restrict__ list, int j) {
-  __shared__ __attribute__((aligned(16))) double lds[GEMM_LDS];
-  const OiCell& c = cells[list[blockIdx.y]];
+// --------------------------------------------------- k_chol_panel(j)
+// One 256-thread workgroup per output tile; logical slots of a cell:
+//   x <  T-1-j : tile (i = j+1+x, j) of the factor, one GEMM loop:
+//                  L_ij^T = sum_{k<j} P_jk L_ik^T + Dinv_jj A_ij^T
+//                (= Dinv_jj (A_ij - sum_k L_ik L_jk^T)^T); slot 0 (i = j+1) then
+//                applies the update of diagonal tile j+1 (look-ahead) for
+//                k_diag_factor(j+1).
+//   x >= T-1-j : (eval) tile (j, jj = x-(T-1-j)) of W = L^-1:
+//                  W_j,jj = sum_{k=jj}^{j-1} P_jk W_k,jj
+__global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ cells,
+                                                   const int32_t* __restrict__ list, int j, int gx,
+                                                   int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
+  int ci, x;
+  if (!xcd_cell_slot(gx, ncell, ci, x)) return;
+  const OiCell& c = cells[list[ci]];
   const int T = c.T;
   if (j >= T || *c.status != OI_OK) return;
   const int ntrsm = T - 1 - j;
-  const int x = blockIdx.x;
+  const double* Pj = c.P;
+  const double* Dj = tileD(c, j);
   Quad acc;
   quad_zero(acc);
   if (x < ntrsm) {
     const int i = j + 1 + x;
-    double* Y = tileL(c, i, j);
-    const double* Dj = tileD(c, j);
-    gemm_kmajor(acc, lds, 1, [&](int, const double*& a, const double*& b) {
-      a = Dj;
-      b = Y;
+    gemm1_kmajor(acc, lds, j + 1, [&](int p, const double*& a, const double*& b) {
+      a = p < j ? Pj + (size_t)p * OI_TILE : Dj;
+      b = tileL(c, i, p);
     });
-    // acc = L_ij^T ; all global reads of Y are complete
+    double* Y = tileL(c, i, j);
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
-        for (int r = 0; r < 4; ++r) Y[acc_row(mb, r) * NB + acc_col(nb)] = acc.c[mb][nb][r];
+        for (int r = 0; r < 4; ++r)
+          Y[acc1_row(mb, r) * NB + acc1_col(nb)] = acc.c[mb][nb][r];  // L_ij, column-major
+    if (x != 0) return;
+    // ---- look-ahead: diagonal tile j+1 = i.
+    // S_d = A_ii - L_ij L_ij^T - sum_{k<j} L_ik L_ik^T; the first product uses
+    // this workgroup's own L_ij, written k-major (X[c][m] = L_ij[m][c] = acc
+    // entry (c, m)) into LDS.
+    double* Xs = lds;
+    for (int mb = 0; mb < 2; ++mb)
+      for (int nb = 0; nb < 2; ++nb)
+        for (int r = 0; r < 4; ++r) Xs[acc1_row(mb, r) * LDSA + acc1_col(nb)] = acc.c[mb][nb][r];
+    __syncthreads();
+    Quad accd;
+    quad_zero(accd);
+    {
+      const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+      const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+#pragma unroll 4
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + fk;
+        const double a0 = Xs[k * LDSA + 32 * wr + fr], a1 = Xs[k * LDSA + 32 * wr + 16 + fr];
+        const double b0 = Xs[k * LDSA + 32 * wc + fr], b1 = Xs[k * LDSA + 32 * wc + 16 + fr];
+        accd.c[0][0] = MFMA64(a0, b0, accd.c[0][0]);
+        accd.c[0][1] = MFMA64(a0, b1, accd.c[0][1]);
+        accd.c[1][0] = MFMA64(a1, b0, accd.c[1][0]);
+        accd.c[1][1] = MFMA64(a1, b1, accd.c[1][1]);
+      }
+    }
+    __syncthreads();
+    gemm1_kmajor(accd, lds, j, [&](int p, const double*& a, const double*& b) {
+      a = tileL(c, i, p);
+      b = a;
+    });
+    double* Yd = tileL(c, i, i);
+    for (int mb = 0; mb < 2; ++mb)
+      for (int nb = 0; nb < 2; ++nb)
+        for (int r = 0; r < 4; ++r) {
+          const int m = acc1_row(mb, r), n = acc1_col(nb);
+          Yd[m * NB + n] = Yd[m * NB + n] - accd.c[mb][nb][r];
+        }
     return;
   }
   const int jj = x - ntrsm;
   if (c.mode != OI_MODE_EVAL || jj >= j) return;
-  // S = sum_{k=jj}^{j-1} L_jk W_k,jj
-  gemm_kmajor(acc, lds, j - jj, [&](int p, const double*& a, const double*& b) {
-    a = tileL(c, j, jj + p);
-    b = tileW(c, jj + p, jj);
+  gemm1_kmajor(acc, lds, j - jj, [&](int p, const double*& a, const double*& b) {
+    const int k = jj + p;
+    a = Pj + (size_t)k * OI_TILE;
+    b = tileW(c, k, jj);
   });
-  // S -> LDS as [k][n] (stride LDSS), then W_j,jj = -Dinv_jj S
-  double* Ss = lds;
-  for (int mb = 0; mb < 2; ++mb)
-    for (int nb = 0; nb < 2; ++nb)
-      for (int r = 0; r < 4; ++r) Ss[acc_row(mb, r) * LDSS + acc_col(nb)] = acc.c[mb][nb][r];
-  __syncthreads();
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  const int fr = lane & 15, fk = lane >> 4;
-  const double* Dj = tileD(c, j);
-  Quad acc2;
-  quad_zero(acc2);
-#pragma unroll 4
-  for (int kk = 0; kk < NB / 4; ++kk) {
-    const int k = kk * 4 + fk;
-    double a0 = Dj[k * NB + 32 * wr + fr];
-    double a1 = Dj[k * NB + 32 * wr + 16 + fr];
-    double b0 = Ss[k * LDSS + 32 * wc + fr];
-    double b1 = Ss[k * LDSS + 32 * wc + 16 + fr];
-    acc2.c[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc2.c[0][0], 0, 0, 0);
-    acc2.c[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc2.c[0][1], 0, 0, 0);
-    acc2.c[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc2.c[1][0], 0, 0, 0);
-    acc2.c[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc2.c[1][1], 0, 0, 0);
-  }
   double* Wt = tileW(c, j, jj);
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
-      for (int r = 0; r < 4; ++r) Wt[acc_row(mb, r) * NB + acc_col(nb)] = -acc2.c[mb][nb][r];
+      for (int r = 0; r < 4; ++r)
+        Wt[acc1_row(mb, r) * NB + acc1_col(nb)] = acc.c[mb][nb][r];  // row-major
 }
 
 // ------------------------------------------------------------- k_zvec
 // z_i = sum_{k<=i} W_ik r_k   (one workgroup per (cell, block row i))
 __global__ __launch_bounds__(256) void k_zvec(const OiCell* __restrict__ cells,
-                                              const int32_t* __restrict__ list) {
-  const OiCell& c = cells[list[blockIdx.y]];
-  const int i = blockIdx.x;
-  if (i >= c.T || *c.status != OI_OK) return;
+                                              const int32_t* __restrict__ list, int gx,
+                                              int ncell) {
+  int ci, i;
+  if (!xcd_cell_slot(gx, ncell, ci, i)) return;
+  const OiCell& c = cells[list[ci]];
+  if (i >= c.T || *c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
   const int t = threadIdx.x, m = t >> 2, q = t & 3, n = c.n;
   double s = 0.0;
   for (int k = 0; k <= i; ++k) {
@@ -391,10 +395,13 @@ __global__ __launch_bounds__(256) void k_zvec(const OiCell* __restrict__ cells,
 // ------------------------------------------------------------- k_avec
 // alpha_k = sum_{i>=k} W_ik^T z_i ; partial r_k . alpha_k
 __global__ __launch_bounds__(256) void k_avec(const OiCell* __restrict__ cells,
-                                              const int32_t* __restrict__ list) {
-  const OiCell& c = cells[list[blockIdx.y]];
-  const int k = blockIdx.x, T = c.T;
-  if (k >= T || *c.status != OI_OK) return;
+                                              const int32_t* __restrict__ list, int gx,
+                                              int ncell) {
+  int ci, k;
+  if (!xcd_cell_slot(gx, ncell, ci, k)) return;
+  const OiCell& c = cells[list[ci]];
+  const int T = c.T;
+  if (k >= T || *c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
   __shared__ double red[4][NB + 1];
   const int t = threadIdx.x, cc = t & 63, mq = t >> 6, n = c.n;
   const double* z = c.vec;
@@ -421,37 +428,44 @@ __global__ __launch_bounds__(256) void k_avec(const OiCell* __restrict__ cells,
 }
 
 // ------------------------------------------------------ k_lauum_grad
-// Tile (i, j) of K^-1 = W^T W  (K^-1_ij = sum_{k>=i} W_ki^T W_kj), fused with
-// sum over the tile of (K^-1 - alpha alpha^T) o {dK_0, dK_1, dK_2, 2K} and its
-// trace (GPR:130-138).  Symmetry: strictly-lower entries count twice.
-__global__ __launch_bounds__(256) void k_lauum_grad(const OiCell* __restrict__ cells,
-                                                    const int32_t* __restrict__ list) {
-  __shared__ __attribute__((aligned(16))) double lds[GEMM_LDS];
-  __shared__ double red[4 * 5];
-  const OiCell& c = cells[list[blockIdx.y]];
+// Tiles (i, j0), (i, j1=j0+1) of K^-1 = W^T W  (K^-1_ij = sum_{k>=i} W_ki^T W_kj)
+// fused with sum over the tiles of (K^-1 - alpha alpha^T) o {dK_0, dK_1, dK_2,
+// 2K} and the trace (GPR:130-138).  Strictly-lower entries count twice.
+__global__ __launch_bounds__(GEMM_THREADS) void k_lauum_grad(const OiCell* __restrict__ cells,
+                                                            const int32_t* __restrict__ list,
+                                                            int gx, int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
+  int ci, slot;
+  if (!xcd_cell_slot(gx, ncell, ci, slot)) return;
+  const OiCell& c = cells[list[ci]];
   const int T = c.T;
-  int i, j;
-  if (!decode_tri(blockIdx.x, T, i, j)) return;
-  if (*c.status != OI_OK) return;
+  int i, J;
+  if (!decode_pair(slot, T, i, J)) return;
+  if (*c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
+  const int j0 = 2 * J, j1 = j0 + 1;
+  const bool has1 = j1 <= i;
   Quad acc;
   quad_zero(acc);
-  gemm_kmajor(acc, lds, T - i, [&](int p, const double*& a, const double*& b) {
-    a = tileW(c, i + p, i);
-    b = tileW(c, i + p, j);
+  gemm2_kmajor(acc, lds, T - i, [&](int p, const double*& a, const double*& b0, const double*& b1) {
+    const int k = i + p;
+    a = tileW(c, k, i);
+    b0 = tileW(c, k, j0);
+    b1 = has1 ? tileW(c, k, j1) : g_zero_tile;
   });
-  // coordinates of the tile's rows (tile i) and columns (tile j), alpha
-  double* uQ = lds;            // [2][3][64] (sqrt3*x)/ell
-  double* uq = lds + 6 * NB;   // [2][3][64] sqrt3*(x/ell)
-  double* al = lds + 12 * NB;  // [2][64]
+  // coordinates of the rows (tile i) and the 128 columns (tiles j0, j1)
+  double* uQ = lds;              // [3][192]: rows 0..63, columns 64..191
+  double* uq = lds + 3 * 192;    // [3][192]
+  double* al = lds + 6 * 192;    // [192]
+  double* red = lds + 7 * 192;   // 8 waves x 5
   const int t = threadIdx.x, n = c.n;
-  if (t < 2 * NB) {
-    int side = t >> 6, idx = t & 63, a = (side ? j : i) * NB + idx;
+  if (t < 192) {
+    const int a = t < 64 ? i * NB + t : j0 * NB + (t - 64);
     for (int d = 0; d < 3; ++d) {
-      double xv = a < n ? c.xyt[3 * a + d] : 0.0;
-      uQ[(side * 3 + d) * NB + idx] = (SQRT3 * xv) / c.hyp[d];
-      uq[(side * 3 + d) * NB + idx] = SQRT3 * (xv / c.hyp[d]);
+      const double xv = a < n ? c.xyt[3 * a + d] : 0.0;
+      uQ[d * 192 + t] = (SQRT3 * xv) / c.hyp[d];
+      uq[d * 192 + t] = SQRT3 * (xv / c.hyp[d]);
     }
-    al[side * NB + idx] = c.vec[T * NB + a];
+    al[t] = a < T * NB ? c.vec[T * NB + a] : 0.0;
   }
   __syncthreads();
   const double sf2 = c.hyp[3];
@@ -459,29 +473,30 @@ __global__ __launch_bounds__(256) void k_lauum_grad(const OiCell* __restrict__ c
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
       for (int r = 0; r < 4; ++r) {
-        const int m = acc_row(mb, r), nn = acc_col(nb);
-        const int a = i * NB + m, b = j * NB + nn;
-        if (a >= n || b >= n || (i == j && m < nn)) continue;
+        const int m = acc_row(mb, r), nc = acc_col(nb);
+        const int jh = nc < 64 ? j0 : j1, nn = nc & 63;
+        const int a = i * NB + m, b = jh * NB + nn;
+        if ((nc >= 64 && !has1) || a >= n || b >= n || (i == jh && m < nn)) continue;
         const double wgt = (a == b) ? 1.0 : 2.0;
-        const double w = acc.c[mb][nb][r] - al[m] * al[NB + nn];
-        double d0 = uQ[0 * NB + m] - uQ[3 * NB + nn];
-        double d1 = uQ[1 * NB + m] - uQ[4 * NB + nn];
-        double d2 = uQ[2 * NB + m] - uQ[5 * NB + nn];
+        const double w = acc.c[mb][nb][r] - al[m] * al[64 + nc];
+        const double d0 = uQ[0 * 192 + m] - uQ[0 * 192 + 64 + nc];
+        const double d1 = uQ[1 * 192 + m] - uQ[1 * 192 + 64 + nc];
+        const double d2 = uQ[2 * 192 + m] - uQ[2 * 192 + 64 + nc];
         const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
         const double e = exp(-Q);
         const double K = sf2 * ((1.0 + Q) * e);
-        double q0 = uq[0 * NB + m] - uq[3 * NB + nn];
-        double q1 = uq[1 * NB + m] - uq[4 * NB + nn];
-        double q2 = uq[2 * NB + m] - uq[5 * NB + nn];
+        const double q0 = uq[0 * 192 + m] - uq[0 * 192 + 64 + nc];
+        const double q1 = uq[1 * 192 + m] - uq[1 * 192 + 64 + nc];
+        const double q2 = uq[2 * 192 + m] - uq[2 * 192 + 64 + nc];
         s[0] += wgt * (w * (sf2 * ((q0 * q0) * e)));
         s[1] += wgt * (w * (sf2 * ((q1 * q1) * e)));
         s[2] += wgt * (w * (sf2 * ((q2 * q2) * e)));
         s[3] += wgt * (w * (2.0 * K));
         if (a == b) s[4] += w;
       }
-  block_sum<5>(s, red);
+  block_sum<5, 8>(s, red);
   if (t == 0) {
-    double* pp = c.part + OI_PART_GRAD(0) + 5 * (size_t)blockIdx.x;
+    double* pp = c.part + OI_PART_GRAD(0) + 5 * (size_t)slot;
     for (int q = 0; q < 5; ++q) pp[q] = s[q];
   }
 }
@@ -494,18 +509,19 @@ __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cel
   if (c.mode != OI_MODE_EVAL) return;
   __shared__ double red[4 * 7];
   const int t = threadIdx.x, T = c.T, ntile = T * (T + 1) / 2;
+  const int nslot = lauum_slots_before(T);
   if (*c.status != OI_OK) {
     if (t < 7) c.out[t] = INFINITY;
     return;
   }
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int x = t; x < ntile; x += 256)
+  for (int x = t; x < nslot; x += 256)
     for (int q = 0; q < 5; ++q) v[q] += c.part[OI_PART_GRAD(ntile) + 5 * x + q];
   for (int k = t; k < T; k += 256) {
     v[5] += c.part[OI_PART_QUAD(ntile) + k];
     v[6] += c.part[OI_PART_LOGDET(ntile, T) + k];
   }
-  block_sum<7>(v, red);
+  block_sum<7, 4>(v, red);
   if (t == 0) {
     const double quad = v[5], logdet = v[6];
     c.out[0] = (quad / 2 + logdet) + (c.n * LOG2PI) / 2;
@@ -624,7 +640,7 @@ __global__ __launch_bounds__(256) void k_predict(const OiCell* __restrict__ cell
     const int bi = a >> 6, bm = a & 63;
     acc5[3] += log(c.L[(((size_t)bi * (bi + 1) / 2) + bi) * OI_TILE + bm * NB + bm]);
   }
-  block_sum<4>(acc5, red);
+  block_sum<4, 4>(acc5, red);
   if (t == 0) {
     c.out[0] = c.mean + acc5[0];
     c.out[1] = sqrt(sf2 - acc5[1]);
@@ -642,68 +658,64 @@ __global__ void k_residual(const double* __restrict__ y, const double* __restric
 // ------------------------------------------------------------ launchers
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 static inline int ret() { return hipGetLastError() == hipSuccess ? 0 : -1; }
-
-#define FOR_CHUNKS(ncell, body)                         \
-  for (int base = 0; base < (ncell); base += 65535) {    \
-    const int cnt = (ncell) - base < 65535 ? (ncell) - base : 65535; \
-    body                                                 \
-  }
+static inline unsigned grid1(int gx, int ncell) { return (unsigned)gx * (unsigned)((ncell + 7) & ~7); }
 
 extern "C" int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                                void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  FOR_CHUNKS(ncell, {
-    hipLaunchKernelGGL(k_build, dim3(maxT * (maxT + 1) / 2, cnt), dim3(256), 0, S(stream), cells,
-                       list + base);
-  })
+  const int gx = maxT * (maxT + 1) / 2;
+  hipLaunchKernelGGL(k_build, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,
+                     ncell);
   return ret();
 }
 
-extern "C" int oi_launch_chol_update(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                                     int j, void* stream) {
-  if (ncell <= 0 || maxT - j <= 0) return 0;
-  FOR_CHUNKS(ncell, {
-    hipLaunchKernelGGL(k_chol_update, dim3(maxT - j, cnt), dim3(256), 0, S(stream), cells,
-                       list + base, j);
-  })
+extern "C" int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j,
+                                     void* stream) {
+  if (ncell <= 0) return 0;
+  hipLaunchKernelGGL(k_diag_factor, dim3(ncell), dim3(64), 0, S(stream), cells, list, j);
   return ret();
 }
 
-extern "C" int oi_launch_trsm_trtri(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                                    int j, void* stream) {
-  if (ncell <= 0 || maxT - 1 <= 0) return 0;
-  FOR_CHUNKS(ncell, {
-    hipLaunchKernelGGL(k_trsm_trtri, dim3(maxT - 1, cnt), dim3(256), 0, S(stream), cells,
-                       list + base, j);
-  })
+extern "C" int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j,
+                               void* stream) {
+  if (ncell <= 0 || j <= 0) return 0;
+  const int gx = (j + SCALE_KPW - 1) / SCALE_KPW;
+  hipLaunchKernelGGL(k_scale, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, gx,
+                     ncell);
+  return ret();
+}
+
+extern "C" int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT,
+                                    int j, int with_trtri, void* stream) {
+  const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
+  if (ncell <= 0 || gx <= 0) return 0;
+  hipLaunchKernelGGL(k_chol_panel, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j,
+                     gx, ncell);
   return ret();
 }
 
 extern "C" int oi_launch_zvec(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                               void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  FOR_CHUNKS(ncell, {
-    hipLaunchKernelGGL(k_zvec, dim3(maxT, cnt), dim3(256), 0, S(stream), cells, list + base);
-  })
+  hipLaunchKernelGGL(k_zvec, dim3(grid1(maxT, ncell)), dim3(256), 0, S(stream), cells, list, maxT,
+                     ncell);
   return ret();
 }
 
 extern "C" int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                               void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  FOR_CHUNKS(ncell, {
-    hipLaunchKernelGGL(k_avec, dim3(maxT, cnt), dim3(256), 0, S(stream), cells, list + base);
-  })
+  hipLaunchKernelGGL(k_avec, dim3(grid1(maxT, ncell)), dim3(256), 0, S(stream), cells, list, maxT,
+                     ncell);
   return ret();
 }
 
 extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                                     void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  FOR_CHUNKS(ncell, {
-    hipLaunchKernelGGL(k_lauum_grad, dim3(maxT * (maxT + 1) / 2, cnt), dim3(256), 0, S(stream),
-                       cells, list + base);
-  })
+  const int gx = lauum_slots_before(maxT);
+  hipLaunchKernelGGL(k_lauum_grad, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
+                     list, gx, ncell);
   return ret();
 }
 
