@@ -129,6 +129,8 @@ KStat g_prof[K_COUNT];
 struct RunStat {
   int64_t rounds = 0, evals = 0, predicts = 0;
   double wall_s = 0.0;
+  double setup_s = 0.0;  // run() entry -> first round (uploads, residuals)
+  double sync_s = 0.0;   // host blocked on round completion
 } g_run;
 struct LaunchRec {
   int kind, j, cells;
@@ -146,6 +148,15 @@ std::vector<RoundRec> g_rounds;  // every profiled round since the last reset
 struct Context {
   int device = 0;
   hipStream_t own_stream = nullptr;
+  std::vector<hipStream_t> aux;  // extra streams for concurrent cell groups
+  hipStream_t aux_stream(int g) {
+    while ((int)aux.size() < g) {
+      hipStream_t s;
+      HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      aux.push_back(s);
+    }
+    return aux[g - 1];
+  }
   Arena arena;
   size_t arena_bytes = 0;
   std::mutex mu;
@@ -288,49 +299,76 @@ int run(const Job& job, const oi_options& o) {
 
   const int cap = (int)std::min<int64_t>(ncell, o.max_pool > 0 ? o.max_pool : 2048);
   std::vector<Slot> slots(cap);
-  std::vector<int> free_slots;
-  for (int s = cap - 1; s >= 0; --s) free_slots.push_back(s);
-  std::vector<int> active;
+
+  // Resident cells are split into G groups with their own stream: while one
+  // group's round runs, the host consumes the other group's results and its
+  // kernels fill the GPU around the first group's latency-bound launches.
+  int G = 1;  // OI_GROUPS=2..8: measured no gain on the day workload (round 1)
+  if (const char* eg = getenv("OI_GROUPS")) G = std::max(1, std::min(8, atoi(eg)));
+  if (cap < 2 * G) G = 1;
+  const int capG = (cap + G - 1) / G;
 
   DBuf d_cells, d_list, d_res, d_stat;
   HBuf h_cells, h_list, h_res, h_stat;
   d_cells.reserve(cap * sizeof(OiCell));
   h_cells.reserve(cap * sizeof(OiCell));
-  d_list.reserve(cap * 4 * 3);
-  h_list.reserve(cap * 4 * 3);
+  d_list.reserve((size_t)G * capG * 4 * 3);
+  h_list.reserve((size_t)G * capG * 4 * 3);
   d_res.reserve(cap * OI_OUT_N * 8);
   h_res.reserve(cap * OI_OUT_N * 8);
   d_stat.reserve(cap * 4);
   h_stat.reserve(cap * 4);
   OiCell* hc = (OiCell*)h_cells.p;
   const OiCell* dc = (const OiCell*)d_cells.p;
-  int32_t* hl = (int32_t*)h_list.p;
-  int32_t* dl = (int32_t*)d_list.p;
   double* hres = (double*)h_res.p;
   int32_t* hst = (int32_t*)h_stat.p;
 
-  // profiling: one start/stop event pair per launch of a round
-  std::vector<hipEvent_t> ev;
-  std::vector<int> ev_kind;
-  if (o.profile) {
-    ev.resize(2 * (2 * 1024 + 16));
-    for (auto& e : ev) HIPC(hipEventCreate(&e));
+  struct Group {
+    int s0 = 0, cap = 0;
+    hipStream_t st = nullptr;
+    std::vector<int> free_slots, active, ev_slots, pr_slots;
+    int32_t* hl = nullptr;  // host lists: all | eval | predict (capG each)
+    int32_t* dl = nullptr;
+    bool inflight = false;
+    int maxT = 0;
+    std::vector<hipEvent_t> ev;
+    std::vector<int> ev_kind;
+    std::vector<std::pair<int, int>> ev_meta;
+  };
+  std::vector<Group> groups(G);
+  hipEvent_t inputs_ready;
+  HIPC(hipEventCreateWithFlags(&inputs_ready, hipEventDisableTiming));
+  HIPC(hipEventRecord(inputs_ready, st));
+  for (int g = 0; g < G; ++g) {
+    Group& gr = groups[g];
+    gr.s0 = g * capG;
+    gr.cap = std::max(0, std::min(capG, cap - g * capG));
+    gr.st = g == 0 ? st : ctx.aux_stream(g);
+    if (g) HIPC(hipStreamWaitEvent(gr.st, inputs_ready, 0));
+    for (int s = gr.s0 + gr.cap - 1; s >= gr.s0; --s) gr.free_slots.push_back(s);
+    gr.hl = (int32_t*)h_list.p + (size_t)g * capG * 3;
+    gr.dl = (int32_t*)d_list.p + (size_t)g * capG * 3;
+    if (o.profile) {
+      gr.ev.resize(2 * (3 * 1024 + 16));
+      for (auto& ee : gr.ev) HIPC(hipEventCreate(&ee));
+    }
   }
   double kms[K_COUNT] = {0}, kfl[K_COUNT] = {0};
   int64_t kln[K_COUNT] = {0};
+  const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
 
   size_t next = 0;
   int64_t rounds = 0, evals = 0, predicts = 0;
-  while (next < order.size() || !active.empty()) {
-    // ---- admission
-    while (next < order.size() && !free_slots.empty()) {
+
+  auto admit = [&](Group& gr) {
+    while (next < order.size() && !gr.free_slots.empty()) {
       const int64_t c = order[next];
       const int64_t n = job.offs[c + 1] - job.offs[c];
       const size_t bytes = cell_bytes(n, eval_mem);
       const size_t off = ctx.arena.alloc(bytes);
       if (off == SIZE_MAX) break;
-      const int s = free_slots.back();
-      free_slots.pop_back();
+      const int s = gr.free_slots.back();
+      gr.free_slots.pop_back();
       Slot& sl = slots[s];
       sl = Slot();
       sl.cell = c;
@@ -375,75 +413,77 @@ int run(const Job& job, const oi_options& o) {
         sl.phase = 2;
         for (int k = 0; k < 5; ++k) sl.hyp[k] = std::exp(job.h[6 * c + k]);
       }
-      active.push_back(s);
+      gr.active.push_back(s);
       ++next;
     }
-    if (active.empty()) return fail(OI_E_NOMEM, "workspace exhausted with no resident cell");
+  };
 
-    // ---- describe this round
-    std::vector<int> ev_slots, pr_slots;
-    for (int s : active) {
+  auto launch_round = [&](Group& gr) {
+    hipStream_t gst = gr.st;
+    gr.ev_slots.clear();
+    gr.pr_slots.clear();
+    for (int s : gr.active) {
       Slot& sl = slots[s];
       OiCell& cd = hc[s];
       if (sl.phase == 0) {
         for (int k = 0; k < 5; ++k) cd.hyp[k] = std::exp(sl.mail.x[k]);  // GPR:120-122
         cd.mode = OI_MODE_EVAL;
-        ev_slots.push_back(s);
+        gr.ev_slots.push_back(s);
       } else if (sl.phase == 2) {
         for (int k = 0; k < 5; ++k) cd.hyp[k] = sl.hyp[k];
         cd.mode = OI_MODE_EVAL;
-        ev_slots.push_back(s);
+        gr.ev_slots.push_back(s);
       } else {
         for (int k = 0; k < 5; ++k) cd.hyp[k] = sl.hyp[k];
         cd.mode = OI_MODE_PREDICT;
-        pr_slots.push_back(s);
+        gr.pr_slots.push_back(s);
       }
     }
     auto byT = [&](std::vector<int>& v) {
       std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return hc[a].T > hc[b].T; });
     };
-    byT(ev_slots);
-    byT(pr_slots);
+    byT(gr.ev_slots);
+    byT(gr.pr_slots);
     std::vector<int> all_slots;
-    all_slots.reserve(active.size());
-    std::merge(ev_slots.begin(), ev_slots.end(), pr_slots.begin(), pr_slots.end(),
+    all_slots.reserve(gr.active.size());
+    std::merge(gr.ev_slots.begin(), gr.ev_slots.end(), gr.pr_slots.begin(), gr.pr_slots.end(),
                std::back_inserter(all_slots), [&](int a, int b) { return hc[a].T > hc[b].T; });
-    const int na = (int)all_slots.size(), ne = (int)ev_slots.size(), np_ = (int)pr_slots.size();
-    int32_t* l_all = hl;
-    int32_t* l_ev = hl + cap;
-    int32_t* l_pr = hl + 2 * cap;
+    const int na = (int)all_slots.size(), ne = (int)gr.ev_slots.size(),
+              np_ = (int)gr.pr_slots.size();
+    int32_t* l_all = gr.hl;
+    int32_t* l_ev = gr.hl + capG;
+    int32_t* l_pr = gr.hl + 2 * capG;
     for (int k = 0; k < na; ++k) l_all[k] = all_slots[k];
-    for (int k = 0; k < ne; ++k) l_ev[k] = ev_slots[k];
-    for (int k = 0; k < np_; ++k) l_pr[k] = pr_slots[k];
+    for (int k = 0; k < ne; ++k) l_ev[k] = gr.ev_slots[k];
+    for (int k = 0; k < np_; ++k) l_pr[k] = gr.pr_slots[k];
     const int maxT = na ? hc[all_slots[0]].T : 0;
-    const int maxTe = ne ? hc[ev_slots[0]].T : 0;
+    const int maxTe = ne ? hc[gr.ev_slots[0]].T : 0;
+    gr.maxT = maxT;
 
-    HIPC(hipMemcpyAsync(d_cells.p, hc, cap * sizeof(OiCell), hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(d_list.p, hl, cap * 4 * 3, hipMemcpyHostToDevice, st));
-    HIPC(hipMemsetAsync(d_stat.p, 0, cap * 4, st));
-    const int32_t* dl_all = dl;
-    const int32_t* dl_ev = dl + cap;
-    const int32_t* dl_pr = dl + 2 * cap;
+    HIPC(hipMemcpyAsync((OiCell*)d_cells.p + gr.s0, hc + gr.s0, gr.cap * sizeof(OiCell),
+                        hipMemcpyHostToDevice, gst));
+    HIPC(hipMemcpyAsync(gr.dl, gr.hl, (size_t)capG * 4 * 3, hipMemcpyHostToDevice, gst));
+    HIPC(hipMemsetAsync((int32_t*)d_stat.p + gr.s0, 0, gr.cap * 4, gst));
+    const int32_t* dl_all = gr.dl;
+    const int32_t* dl_ev = gr.dl + capG;
+    const int32_t* dl_pr = gr.dl + 2 * capG;
 
-    // executed tile-GEMM flops per kernel (profile only)
-    const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
-    ev_kind.clear();
-    std::vector<std::pair<int, int>> ev_meta;  // (j, cells) per launch
+    gr.ev_kind.clear();
+    gr.ev_meta.clear();
     int cur_j = -1, cur_cells = 0;
     auto mark = [&](int k, bool end) {
       if (!o.profile) return;
       if (!end) {
-        ev_kind.push_back(k);
-        ev_meta.emplace_back(cur_j, cur_cells);
+        gr.ev_kind.push_back(k);
+        gr.ev_meta.emplace_back(cur_j, cur_cells);
       }
-      const size_t idx = 2 * (ev_kind.size() - 1) + (end ? 1 : 0);
-      if (idx < ev.size()) HIPC(hipEventRecord(ev[idx], st));
+      const size_t idx = 2 * (gr.ev_kind.size() - 1) + (end ? 1 : 0);
+      if (idx < gr.ev.size()) HIPC(hipEventRecord(gr.ev[idx], gst));
     };
-    // ---- launch sequence
     int rc = 0;
     cur_cells = na;
     mark(K_BUILD, false);
-    rc |= oi_launch_build(dc, dl_all, na, maxT, st);
+    rc |= oi_launch_build(dc, dl_all, na, maxT, gst);
     mark(K_BUILD, true);
     for (int j = 0; j < maxT; ++j) {
       int cnt = 0;
@@ -451,15 +491,15 @@ int run(const Job& job, const oi_options& o) {
       cur_j = j;
       cur_cells = cnt;
       mark(K_CHOL, false);
-      rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, st);
+      rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, gst);
       mark(K_CHOL, true);
       mark(K_SCALE, false);
-      rc |= oi_launch_scale(dc, dl_all, cnt, j, st);
+      rc |= oi_launch_scale(dc, dl_all, cnt, j, gst);
       mark(K_SCALE, true);
       mark(K_TRSM, false);
-      rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, st);
+      rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
       mark(K_TRSM, true);
-      if (o.profile) {  // executed MFMA flops: each workgroup = 64 x 128 products
+      if (o.profile) {  // executed MFMA flops: 2*64^3 per 64x64 tile product
         for (int k = 0; k < cnt; ++k) {
           const OiCell& cd = hc[all_slots[k]];
           kfl[K_SCALE] += tf * (double)j;
@@ -473,52 +513,61 @@ int run(const Job& job, const oi_options& o) {
     cur_j = -1;
     cur_cells = ne;
     mark(K_ZVEC, false);
-    rc |= oi_launch_zvec(dc, dl_ev, ne, maxTe, st);
+    rc |= oi_launch_zvec(dc, dl_ev, ne, maxTe, gst);
     mark(K_ZVEC, true);
     mark(K_AVEC, false);
-    rc |= oi_launch_avec(dc, dl_ev, ne, maxTe, st);
+    rc |= oi_launch_avec(dc, dl_ev, ne, maxTe, gst);
     mark(K_AVEC, true);
     mark(K_LAUUM, false);
-    rc |= oi_launch_lauum_grad(dc, dl_ev, ne, maxTe, st);
+    rc |= oi_launch_lauum_grad(dc, dl_ev, ne, maxTe, gst);
     mark(K_LAUUM, true);
     mark(K_FINAL, false);
-    rc |= oi_launch_finalize(dc, dl_ev, ne, st);
+    rc |= oi_launch_finalize(dc, dl_ev, ne, gst);
     mark(K_FINAL, true);
+    cur_cells = np_;
     mark(K_PRED, false);
-    rc |= oi_launch_predict(dc, dl_pr, np_, st);
+    rc |= oi_launch_predict(dc, dl_pr, np_, gst);
     mark(K_PRED, true);
     if (rc) throw HipError(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    HIPC(hipMemcpyAsync(h_res.p, d_res.p, cap * OI_OUT_N * 8, hipMemcpyDeviceToHost, st));
-    HIPC(hipMemcpyAsync(h_stat.p, d_stat.p, cap * 4, hipMemcpyDeviceToHost, st));
-    HIPC(hipStreamSynchronize(st));
+    HIPC(hipMemcpyAsync(hres + (size_t)gr.s0 * OI_OUT_N, (double*)d_res.p + (size_t)gr.s0 * OI_OUT_N,
+                        (size_t)gr.cap * OI_OUT_N * 8, hipMemcpyDeviceToHost, gst));
+    HIPC(hipMemcpyAsync(hst + gr.s0, (int32_t*)d_stat.p + gr.s0, (size_t)gr.cap * 4,
+                        hipMemcpyDeviceToHost, gst));
+    if (o.profile) {
+      for (int k = 0; k < ne; ++k) {
+        const OiCell& cd = hc[gr.ev_slots[k]];
+        for (int i = 0; i < cd.T; ++i) kfl[K_LAUUM] += tf * (double)(cd.T - i) * (i + 1);
+      }
+    }
+    gr.inflight = true;
+  };
+
+  double sync_s = 0.0;
+  auto consume = [&](Group& gr) {
+    const auto ts0 = std::chrono::steady_clock::now();
+    HIPC(hipStreamSynchronize(gr.st));
+    sync_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts0).count();
+    gr.inflight = false;
     ++rounds;
     if (o.profile) {
       std::vector<LaunchRec> recs;
-      for (size_t q = 0; q < ev_kind.size() && 2 * q + 1 < ev.size(); ++q) {
+      for (size_t q = 0; q < gr.ev_kind.size() && 2 * q + 1 < gr.ev.size(); ++q) {
         float a = 0;
-        HIPC(hipEventElapsedTime(&a, ev[2 * q], ev[2 * q + 1]));
-        kms[ev_kind[q]] += a;
-        kln[ev_kind[q]]++;
-        recs.push_back({ev_kind[q], ev_meta[q].first, ev_meta[q].second, (double)a});
+        HIPC(hipEventElapsedTime(&a, gr.ev[2 * q], gr.ev[2 * q + 1]));
+        kms[gr.ev_kind[q]] += a;
+        kln[gr.ev_kind[q]]++;
+        recs.push_back({gr.ev_kind[q], gr.ev_meta[q].first, gr.ev_meta[q].second, (double)a});
       }
       double rms = 0.0, work = 0.0;
       for (const auto& rr : recs) rms += rr.ms;
-      for (int k = 0; k < ne; ++k) work += std::pow((double)hc[ev_slots[k]].T, 3.0);
-      {
-        std::lock_guard<std::mutex> pl(g_prof_mu);
-        g_last_round.swap(recs);
-        g_rounds.push_back({ne, np_, maxT, work, rms});
-      }
-      for (int k = 0; k < ne; ++k) {
-        const OiCell& cd = hc[ev_slots[k]];
-        for (int i = 0; i < cd.T; ++i) kfl[K_LAUUM] += 2 * tf * (double)(cd.T - i) * (i / 2 + 1);
-      }
+      for (int s : gr.ev_slots) work += std::pow((double)hc[s].T, 3.0);
+      std::lock_guard<std::mutex> pl(g_prof_mu);
+      g_last_round.swap(recs);
+      g_rounds.push_back({(int)gr.ev_slots.size(), (int)gr.pr_slots.size(), gr.maxT, work, rms});
     }
-
-    // ---- consume results
     std::vector<int> still;
-    still.reserve(active.size());
-    for (int s : active) {
+    still.reserve(gr.active.size());
+    for (int s : gr.active) {
       Slot& sl = slots[s];
       const double* rr = hres + (size_t)s * OI_OUT_N;
       const int64_t c = sl.cell;
@@ -564,15 +613,37 @@ int run(const Job& job, const oi_options& o) {
         ctx.arena.release(sl.off, sl.bytes);
         sl.task = oi::Task<oi::CgResult>();
         sl.cell = -1;
-        free_slots.push_back(s);
+        gr.free_slots.push_back(s);
       } else {
         still.push_back(s);
       }
     }
-    active.swap(still);
+    gr.active.swap(still);
+  };
+
+  const double setup_s =
+      std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+  while (true) {
+    bool any = false;
+    for (Group& gr : groups) {
+      if (gr.inflight) consume(gr);
+      admit(gr);
+      if (!gr.active.empty()) {
+        launch_round(gr);
+        any = true;
+      }
+    }
+    if (!any) {
+      if (next < order.size()) return fail(OI_E_NOMEM, "workspace exhausted with no resident cell");
+      break;
+    }
+  }
+  (void)hipEventDestroy(inputs_ready);
+  if (o.profile) {
+    for (Group& gr : groups)
+      for (auto& ee : gr.ev) (void)hipEventDestroy(ee);
   }
   if (o.profile) {
-    for (auto& e : ev) (void)hipEventDestroy(e);
     std::lock_guard<std::mutex> pl(g_prof_mu);
     for (int k = 0; k < K_COUNT; ++k) {
       g_prof[k].launches += kln[k];
@@ -585,6 +656,8 @@ int run(const Job& job, const oi_options& o) {
     g_run.rounds += rounds;
     g_run.evals += evals;
     g_run.predicts += predicts;
+    g_run.setup_s += setup_s;
+    g_run.sync_s += sync_s;
     g_run.wall_s +=
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
   }

@@ -141,38 +141,43 @@ __device__ __forceinline__ int acc1_col(int nb) {
   return 32 * (w & 1) + 16 * nb + (lane & 15);
 }
 
+// Staging registers are a two-deep ring (chunks ch+1 and ch+2 in flight while
+// ch is multiplied out of LDS): 66 TF/s vs 57 TF/s for a one-deep prefetch
+// when one operand is L2-resident (tools/gemm_probe3.hip).  Native vector
+// types (not HIP's double2 struct) keep the ring in VGPRs.
+typedef double dv2 __attribute__((ext_vector_type(2)));
+struct StageRegs {
+  dv2 a0, a1, b0, b1;
+};
+
 template <class PairFn>
 __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = w >> 1, wc = w & 1;
-  const int nch = npairs * (GNB / KC);
+  const int nch = npairs * (GNB / KC);  // even
   if (nch == 0) return;
   const int sk = t >> 4, sm = (t & 15) * 4;
-  double2 ra0, ra1, rb0, rb1;
-  auto load = [&](int ch) {
+  const int fr = lane & 15, fk = lane >> 4;
+  StageRegs r0, r1;
+  auto load = [&](int ch, StageRegs& q) __attribute__((always_inline)) {
     const double *pa, *pb;
     pair(ch >> 2, pa, pb);
     const int off = (ch & 3) * KC * GNB + t * 4;
-    ra0 = *(const double2*)(pa + off);
-    ra1 = *(const double2*)(pa + off + 2);
-    rb0 = *(const double2*)(pb + off);
-    rb1 = *(const double2*)(pb + off + 2);
+    q.a0 = *(const dv2*)(pa + off);
+    q.a1 = *(const dv2*)(pa + off + 2);
+    q.b0 = *(const dv2*)(pb + off);
+    q.b1 = *(const dv2*)(pb + off + 2);
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const StageRegs& q) __attribute__((always_inline)) {
     double* As = lds + buf * 2 * STAGE_A;
     double* Bs = As + STAGE_A;
-    *(double2*)(As + sk * LDSA + sm) = ra0;
-    *(double2*)(As + sk * LDSA + sm + 2) = ra1;
-    *(double2*)(Bs + sk * LDSA + sm) = rb0;
-    *(double2*)(Bs + sk * LDSA + sm + 2) = rb1;
+    *(dv2*)(As + sk * LDSA + sm) = q.a0;
+    *(dv2*)(As + sk * LDSA + sm + 2) = q.a1;
+    *(dv2*)(Bs + sk * LDSA + sm) = q.b0;
+    *(dv2*)(Bs + sk * LDSA + sm + 2) = q.b1;
   };
-  load(0);
-  store(0);
-  __syncthreads();
-  const int fr = lane & 15, fk = lane >> 4;
-  for (int ch = 0; ch < nch; ++ch) {
-    if (ch + 1 < nch) load(ch + 1);
-    const double* As = lds + (ch & 1) * 2 * STAGE_A;
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const double* As = lds + buf * 2 * STAGE_A;
     const double* Bs = As + STAGE_A;
 #pragma unroll
     for (int kk = 0; kk < KC / 4; ++kk) {
@@ -186,7 +191,19 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs,
       acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
       acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
     }
-    if (ch + 1 < nch) store((ch + 1) & 1);
+  };
+  load(0, r0);
+  load(1, r1);
+  store(0, r0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ch += 2) {
+    if (ch + 2 < nch) load(ch + 2, r0);
+    compute(0);
+    store(1, r1);
+    __syncthreads();
+    if (ch + 3 < nch) load(ch + 3, r1);
+    compute(1);
+    if (ch + 2 < nch) store(0, r0);
     __syncthreads();
   }
 }

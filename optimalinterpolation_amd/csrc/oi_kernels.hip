@@ -25,6 +25,7 @@
 // cell's results are bitwise independent of the batch it runs in.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "oi_device.h"
 #include "oi_gemm.h"
@@ -376,20 +377,30 @@ __global__ __launch_bounds__(256) void k_zvec(const OiCell* __restrict__ cells,
   if (!xcd_cell_slot(gx, ncell, ci, i)) return;
   const OiCell& c = cells[list[ci]];
   if (i >= c.T || *c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
-  const int t = threadIdx.x, m = t >> 2, q = t & 3, n = c.n;
-  double s = 0.0;
-  for (int k = 0; k <= i; ++k) {
-    const double* Wt = tileW(c, i, k) + m * NB + 16 * q;
-    const int b0 = k * NB + 16 * q;
+  // lane pair (t & 31) covers columns 2(t&31), +1 of rows 8p + (t >> 5):
+  // each load instruction reads two whole 512 B rows (coalesced).
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  const int t = threadIdx.x, h = t >> 5, cp = (t & 31) * 2, n = c.n;
+  double s[8];
 #pragma unroll
-    for (int cc = 0; cc < 16; ++cc) {
-      const int b = b0 + cc;
-      s += Wt[cc] * (b < n ? c.r[b] : 0.0);
+  for (int p = 0; p < 8; ++p) s[p] = 0.0;
+  for (int k = 0; k <= i; ++k) {
+    const int b = k * NB + cp;
+    const double r0 = b < n ? c.r[b] : 0.0, r1 = b + 1 < n ? c.r[b + 1] : 0.0;
+    const double* Wt = tileW(c, i, k) + cp;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const dv2 w = *(const dv2*)(Wt + (8 * p + h) * NB);
+      s[p] = fma(w.y, r1, fma(w.x, r0, s[p]));
     }
   }
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  if (q == 0) c.vec[i * NB + m] = s;
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+    for (int o = 16; o >= 1; o >>= 1) s[p] += __shfl_xor(s[p], o, 64);
+  if ((t & 31) == 0) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) c.vec[i * NB + 8 * p + h] = s[p];
+  }
 }
 
 // ------------------------------------------------------------- k_avec
@@ -501,15 +512,82 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_lauum_grad(const OiCell* __res
   }
 }
 
+// One-tile variant (256 threads, 40 KiB LDS -> 4 workgroups per CU): tile
+// (i, j) of K^-1 = sum_{k>=i} W_ki^T W_kj fused with the same gradient sums.
+__global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ cells,
+                                                    const int32_t* __restrict__ list, int gx,
+                                                    int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
+  int ci, tile;
+  if (!xcd_cell_slot(gx, ncell, ci, tile)) return;
+  const OiCell& c = cells[list[ci]];
+  const int T = c.T;
+  int i, j;
+  if (!decode_tri(tile, T, i, j)) return;
+  if (*c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
+  Quad acc;
+  quad_zero(acc);
+  gemm1_kmajor(acc, lds, T - i, [&](int p, const double*& a, const double*& b) {
+    a = tileW(c, i + p, i);
+    b = tileW(c, i + p, j);
+  });
+  double* uQ = lds;            // [3][128]: rows 0..63, columns 64..127
+  double* uq = lds + 3 * 128;  // [3][128]
+  double* al = lds + 6 * 128;  // [128]
+  double* red = lds + 7 * 128;
+  const int t = threadIdx.x, n = c.n;
+  if (t < 128) {
+    const int a = t < 64 ? i * NB + t : j * NB + (t - 64);
+    for (int d = 0; d < 3; ++d) {
+      const double xv = a < n ? c.xyt[3 * a + d] : 0.0;
+      uQ[d * 128 + t] = (SQRT3 * xv) / c.hyp[d];
+      uq[d * 128 + t] = SQRT3 * (xv / c.hyp[d]);
+    }
+    al[t] = c.vec[T * NB + a];
+  }
+  __syncthreads();
+  const double sf2 = c.hyp[3];
+  double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb)
+      for (int r = 0; r < 4; ++r) {
+        const int m = acc1_row(mb, r), nn = acc1_col(nb);
+        const int a = i * NB + m, b = j * NB + nn;
+        if (a >= n || b >= n || (i == j && m < nn)) continue;
+        const double wgt = (a == b) ? 1.0 : 2.0;
+        const double w = acc.c[mb][nb][r] - al[m] * al[64 + nn];
+        const double d0 = uQ[0 * 128 + m] - uQ[0 * 128 + 64 + nn];
+        const double d1 = uQ[1 * 128 + m] - uQ[1 * 128 + 64 + nn];
+        const double d2 = uQ[2 * 128 + m] - uQ[2 * 128 + 64 + nn];
+        const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        const double e = exp(-Q);
+        const double K = sf2 * ((1.0 + Q) * e);
+        const double q0 = uq[0 * 128 + m] - uq[0 * 128 + 64 + nn];
+        const double q1 = uq[1 * 128 + m] - uq[1 * 128 + 64 + nn];
+        const double q2 = uq[2 * 128 + m] - uq[2 * 128 + 64 + nn];
+        s[0] += wgt * (w * (sf2 * ((q0 * q0) * e)));
+        s[1] += wgt * (w * (sf2 * ((q1 * q1) * e)));
+        s[2] += wgt * (w * (sf2 * ((q2 * q2) * e)));
+        s[3] += wgt * (w * (2.0 * K));
+        if (a == b) s[4] += w;
+      }
+  block_sum<5, 4>(s, red);
+  if (t == 0) {
+    double* pp = c.part + OI_PART_GRAD(0) + 5 * (size_t)tile;
+    for (int q = 0; q < 5; ++q) pp[q] = s[q];
+  }
+}
+
 // ---------------------------------------------------------- k_finalize
 // nlZ = r.alpha/2 + sum log diag L + n log(2 pi)/2 (GPR:128); dnlZ (GPR:131-138)
 __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cells,
-                                                  const int32_t* __restrict__ list) {
+                                                  const int32_t* __restrict__ list,
+                                                  int one_tile_slots) {
   const OiCell& c = cells[list[blockIdx.x]];
   if (c.mode != OI_MODE_EVAL) return;
   __shared__ double red[4 * 7];
   const int t = threadIdx.x, T = c.T, ntile = T * (T + 1) / 2;
-  const int nslot = lauum_slots_before(T);
+  const int nslot = one_tile_slots ? ntile : lauum_slots_before(T);
   if (*c.status != OI_OK) {
     if (t < 7) c.out[t] = INFINITY;
     return;
@@ -658,6 +736,15 @@ __global__ void k_residual(const double* __restrict__ y, const double* __restric
 // ------------------------------------------------------------ launchers
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 static inline int ret() { return hipGetLastError() == hipSuccess ? 0 : -1; }
+// lauum variant: one-tile 256-thread kernel (default, OI_LAUUM=1) or the
+// two-tile 512-thread kernel (OI_LAUUM=0); measured equal within 3 % on the day
+static inline bool lauum_one_tile() {
+  static const int v = [] {
+    const char* e = getenv("OI_LAUUM");
+    return e ? atoi(e) : 1;
+  }();
+  return v == 1;
+}
 static inline unsigned grid1(int gx, int ncell) { return (unsigned)gx * (unsigned)((ncell + 7) & ~7); }
 
 extern "C" int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT,
@@ -713,9 +800,15 @@ extern "C" int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncel
 extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                                     void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  const int gx = lauum_slots_before(maxT);
-  hipLaunchKernelGGL(k_lauum_grad, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
-                     list, gx, ncell);
+  if (lauum_one_tile()) {
+    const int gx = maxT * (maxT + 1) / 2;
+    hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list,
+                       gx, ncell);
+  } else {
+    const int gx = lauum_slots_before(maxT);
+    hipLaunchKernelGGL(k_lauum_grad, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream),
+                       cells, list, gx, ncell);
+  }
   return ret();
 }
 
@@ -729,7 +822,8 @@ extern "C" int oi_launch_predict(const OiCell* cells, const int32_t* list, int n
 extern "C" int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell,
                                   void* stream) {
   if (ncell <= 0) return 0;
-  hipLaunchKernelGGL(k_finalize, dim3(ncell), dim3(256), 0, S(stream), cells, list);
+  hipLaunchKernelGGL(k_finalize, dim3(ncell), dim3(256), 0, S(stream), cells, list,
+                     lauum_one_tile() ? 1 : 0);
   return ret();
 }
 

@@ -9,3 +9,5 @@ timeout -k 10 400 python bench.py --steps 1 --warmup 0 --no-cpu-baseline --out g
 python -c "
 import json; d=json.load(open('gpurun_out/bench_iter.json'))
 r=d['roofline']; print('value', d['value'], 'cells/s; evals/cell', d['evals_per_cell'], '; useful TF', r['useful_tflops_per_gpu'], '; dom', r['kernel'], r['achieved'], 'TF'); print(r['kernels_ms'])"
+timeout -k 10 300 python scripts/round_perf.py > gpurun_out/round.log 2>&1 || { tail -30 gpurun_out/round.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/round.log
