@@ -210,11 +210,13 @@ def main():
     tfile = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tfile):
         try:
-            traffic = json.load(open(tfile)).get(dom, {}).get('hbm_bytes_per_launch')
+            traffic = json.load(open(tfile)).get(dom, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
+                "traffic_note": ("HBM bytes per launch of this kernel, rocprofv3 PMC FETCH_SIZE(x2, gfx950)+WRITE_SIZE, "
+                                 "profiles/pmc_traffic.json") if traffic is not None else None,
                 "launches": kd['launches'], "avg_launch_ms": kd['total_ms'] / max(kd['launches'], 1),
                 "flops_per_launch": kd['flops'] / max(kd['launches'], 1),
                 "flop_model": "executed fp64 MFMA tile products, 2*64^3 each (padded tiles)",
