@@ -85,6 +85,39 @@ int oi_nlml_grad_batch(const double* xyt, const double* y, const double* mX,
                        const int64_t* offs, int64_t ncell, const double* h, double* nlz,
                        double* grad, int32_t* status, const oi_options* opts);
 
+/* ---- day pipeline: the steps either side of the per-cell loops ----------
+ * With opts->device_inputs = 1 every array argument below is a DEVICE pointer
+ * on opts->device except vmax, kern and offs, which are always host arrays. */
+
+/* smooth() (GPR:65-76) of nf fields at once -- the five calls GPR:303-307.
+ *   fields [nf x ny x nx]  (the reference's 2-D grids, row-major)
+ *   vmax   [nf]            clip values (GPR:303-307: 2*radius*1000, .., T, 0.1, 0.05)
+ *   mask   [ny x nx]       SIE grid; NaN entries are set to NaN in the output
+ *   kern   [ks x ks] or NULL: the Gaussian2DKernel(x_stddev=std) array; NULL =>
+ *                          built here from std (astropy's definition)
+ *   out    [nf x ny x nx]
+ * inf -> NaN, clip at vmax, astropy convolve() defaults (fill 0 boundary,
+ * NaN-interpolating renormalised kernel), zeros -> np.nanmean, mask. */
+int oi_smooth_fields(const double* fields, int32_t nf, int64_t ny, int64_t nx, const double* vmax,
+                     const double* mask, double std, const double* kern, int32_t ks, double* out,
+                     const oi_options* opts);
+
+/* X_tree.query_ball_point(X[index], r) (GPR:159) for Q targets at once.
+ *   pts [M x 2] training (x, y); q [Q x 2] targets; r radius (same units)
+ *   offs [Q+1] (host) always written: target k owns idx[offs[k] .. offs[k+1])
+ *   idx  [cap] written only when cap >= offs[Q] (call once with idx = NULL to
+ *        size it).  Indices ascending within a target (sorted(ID)); the test
+ *        is scipy cKDTree's p=2 one: (dx*dx + dy*dy) <= r*r. */
+int oi_ball_query(const double* pts, int64_t M, const double* q, int64_t Q, double r,
+                  int64_t* offs, int64_t* idx, int64_t cap, const oi_options* opts);
+
+/* inputs = [x_train, y_train, t_train][ID], outputs = z[ID] (GPR:160-161) for a
+ * ragged index list (e.g. oi_ball_query's idx): xyt [N x 3], zout [N].
+ * Out-of-range indices are an OI_E_ARG error (host mode) or NaN rows (device). */
+int oi_gather_rows(const double* x_train, const double* y_train, const double* t_train,
+                   const double* z, int64_t M, const int64_t* idx, int64_t N, double* xyt,
+                   double* zout, const oi_options* opts);
+
 /* ---- host optimiser (scipy 1.15 CG restated; see csrc/cg.hpp) ---- */
 typedef struct oi_cg oi_cg;
 /* x0: 6 log-hypers. gtol/maxiter as in oi_options (maxiter < 0 => 1200). */

@@ -32,7 +32,8 @@ c_int32_p = ctypes.POINTER(ctypes.c_int32)
 # every symbol include/oi.h declares (tests/test_abi.py checks the export list)
 EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_create',
            'oi_cg_step', 'oi_cg_feed', 'oi_cg_result', 'oi_cg_destroy', 'oi_last_error',
-           'oi_version', 'oi_profile_json', 'oi_profile_reset')
+           'oi_version', 'oi_profile_json', 'oi_profile_reset', 'oi_smooth_fields',
+           'oi_ball_query', 'oi_gather_rows')
 
 
 class OiOptions(ctypes.Structure):
@@ -84,6 +85,18 @@ def load():
         lib.oi_profile_json.restype = ctypes.c_int64
         lib.oi_profile_reset.argtypes = []
         lib.oi_profile_reset.restype = None
+        lib.oi_smooth_fields.argtypes = [c_double_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                                         c_double_p, c_double_p, ctypes.c_double, c_double_p,
+                                         ctypes.c_int32, c_double_p, ctypes.POINTER(OiOptions)]
+        lib.oi_smooth_fields.restype = ctypes.c_int
+        lib.oi_ball_query.argtypes = [c_double_p, ctypes.c_int64, c_double_p, ctypes.c_int64,
+                                      ctypes.c_double, c_int64_p, c_int64_p, ctypes.c_int64,
+                                      ctypes.POINTER(OiOptions)]
+        lib.oi_ball_query.restype = ctypes.c_int
+        lib.oi_gather_rows.argtypes = [c_double_p, c_double_p, c_double_p, c_double_p, ctypes.c_int64,
+                                       c_int64_p, ctypes.c_int64, c_double_p, c_double_p,
+                                       ctypes.POINTER(OiOptions)]
+        lib.oi_gather_rows.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -235,6 +248,116 @@ class CG:
         if getattr(self, '_h', None):
             self._lib.oi_cg_destroy(self._h)
             self._h = None
+
+
+def _dptr(t, ctype=ctypes.c_double):
+    """Device pointer of a torch tensor (plumbing for device_inputs=1 calls)."""
+    if not t.is_contiguous():
+        raise ValueError("device arrays must be contiguous")
+    return ctypes.cast(t.data_ptr(), ctypes.POINTER(ctype))
+
+
+def smooth_fields(fields, vmax, mask, kern, **opt_kw):
+    """oi_smooth_fields (GPR:65-76 for nf fields): fields [nf, ny, nx] host
+    arrays; kern the Gaussian2DKernel array (odd square).  Returns [nf, ny, nx]."""
+    lib = load()
+    f = np.ascontiguousarray(fields, dtype=np.float64)
+    if f.ndim == 2:
+        f = f[None]
+    nf, ny, nx = f.shape
+    vm = np.ascontiguousarray(np.broadcast_to(np.asarray(vmax, dtype=np.float64), (nf,)))
+    m = np.ascontiguousarray(mask, dtype=np.float64)
+    k = np.ascontiguousarray(kern, dtype=np.float64)
+    if m.shape != (ny, nx) or k.ndim != 2 or k.shape[0] != k.shape[1] or k.shape[0] % 2 != 1:
+        raise ValueError("mask must be [ny, nx] and kern an odd square")
+    out = np.empty_like(f)
+    _check(lib.oi_smooth_fields(_ptr(f, ctypes.c_double), nf, ny, nx, _ptr(vm, ctypes.c_double),
+                                _ptr(m, ctypes.c_double), 0.0, _ptr(k, ctypes.c_double), k.shape[0],
+                                _ptr(out, ctypes.c_double), ctypes.byref(options(**opt_kw))))
+    return out
+
+
+def smooth_fields_device(fields_dev, vmax, mask_dev, kern, out_dev, **opt_kw):
+    """oi_smooth_fields on HBM-resident tensors ([nf, ny, nx] fp64 in and out)."""
+    lib = load()
+    nf, ny, nx = fields_dev.shape
+    if tuple(mask_dev.shape) != (ny, nx) or tuple(out_dev.shape) != (nf, ny, nx):
+        raise ValueError("shape mismatch")
+    vm = np.ascontiguousarray(np.broadcast_to(np.asarray(vmax, dtype=np.float64), (nf,)))
+    k = np.ascontiguousarray(kern, dtype=np.float64)
+    _check(lib.oi_smooth_fields(_dptr(fields_dev), nf, ny, nx, _ptr(vm, ctypes.c_double),
+                                _dptr(mask_dev), 0.0, _ptr(k, ctypes.c_double), k.shape[0],
+                                _dptr(out_dev), ctypes.byref(options(device_inputs=True, **opt_kw))))
+    return out_dev
+
+
+def ball_query(pts, q, r, **opt_kw):
+    """oi_ball_query on host arrays: returns (offs [Q+1], idx [offs[-1]])."""
+    lib = load()
+    P = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 2)
+    Qa = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, 2)
+    offs = np.zeros(len(Qa) + 1, dtype=np.int64)
+    o = options(**opt_kw)
+    _check(lib.oi_ball_query(_ptr(P, ctypes.c_double), len(P), _ptr(Qa, ctypes.c_double), len(Qa),
+                             float(r), _ptr(offs, ctypes.c_int64), None, 0, ctypes.byref(o)))
+    idx = np.empty(int(offs[-1]), dtype=np.int64)
+    if len(idx):
+        _check(lib.oi_ball_query(_ptr(P, ctypes.c_double), len(P), _ptr(Qa, ctypes.c_double),
+                                 len(Qa), float(r), _ptr(offs, ctypes.c_int64),
+                                 _ptr(idx, ctypes.c_int64), len(idx), ctypes.byref(o)))
+    return offs, idx
+
+
+def ball_query_device(pts_dev, q_dev, r, counts_only=False, **opt_kw):
+    """oi_ball_query on HBM-resident [M, 2] / [Q, 2] tensors: returns
+    (offs host [Q+1], idx device int64 tensor, or None with counts_only)."""
+    import torch
+    lib = load()
+    M, Q = pts_dev.shape[0], q_dev.shape[0]
+    offs = np.zeros(Q + 1, dtype=np.int64)
+    o = options(device_inputs=True, **opt_kw)
+    _check(lib.oi_ball_query(_dptr(pts_dev), M, _dptr(q_dev), Q, float(r),
+                             _ptr(offs, ctypes.c_int64), None, 0, ctypes.byref(o)))
+    if counts_only:
+        return offs, None
+    idx = torch.empty(int(offs[-1]), dtype=torch.int64, device=pts_dev.device)
+    if idx.numel():
+        _check(lib.oi_ball_query(_dptr(pts_dev), M, _dptr(q_dev), Q, float(r),
+                                 _ptr(offs, ctypes.c_int64), _dptr(idx, ctypes.c_int64),
+                                 idx.numel(), ctypes.byref(o)))
+    return offs, idx
+
+
+def gather_rows(x_train, y_train, t_train, z, idx, **opt_kw):
+    """oi_gather_rows on host arrays: returns (xyt [N, 3], z [N])."""
+    lib = load()
+    cols = [np.ascontiguousarray(a, dtype=np.float64) for a in (x_train, y_train, t_train, z)]
+    M = len(cols[0])
+    if any(len(c) != M for c in cols):
+        raise ValueError("training columns differ in length")
+    I = np.ascontiguousarray(idx, dtype=np.int64)
+    xyt = np.empty((len(I), 3))
+    zo = np.empty(len(I))
+    _check(lib.oi_gather_rows(*[_ptr(c, ctypes.c_double) for c in cols], M, _ptr(I, ctypes.c_int64),
+                              len(I), _ptr(xyt, ctypes.c_double), _ptr(zo, ctypes.c_double),
+                              ctypes.byref(options(**opt_kw))))
+    return xyt, zo
+
+
+def gather_rows_device(cols_dev, idx_dev, **opt_kw):
+    """oi_gather_rows on HBM-resident tensors: cols_dev = (x, y, t, z) [M] each;
+    returns (xyt [N, 3], z [N]) device tensors."""
+    import torch
+    lib = load()
+    M = cols_dev[0].numel()
+    N = idx_dev.numel()
+    xyt = torch.empty((N, 3), dtype=torch.float64, device=idx_dev.device)
+    zo = torch.empty(N, dtype=torch.float64, device=idx_dev.device)
+    if N:
+        _check(lib.oi_gather_rows(*[_dptr(c) for c in cols_dev], M, _dptr(idx_dev, ctypes.c_int64), N,
+                                  _dptr(xyt), _dptr(zo),
+                                  ctypes.byref(options(device_inputs=True, **opt_kw))))
+    return xyt, zo
 
 
 def profile_json():

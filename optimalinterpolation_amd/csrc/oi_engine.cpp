@@ -822,6 +822,8 @@ int oi_cg_result(oi_cg* h, double* x, double* fun, int32_t* nit, int32_t* status
 void oi_cg_destroy(oi_cg* h) { delete h; }
 
 const char* oi_last_error(void) { return g_last_error.c_str(); }
+// internal: lets the other translation units (oi_day.cpp) report errors
+int oi_set_last_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
 int32_t oi_version(void) { return OI_VERSION; }
 
 int64_t oi_profile_json(char* buf, int64_t len) {

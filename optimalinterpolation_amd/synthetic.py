@@ -110,3 +110,39 @@ def make_day(seed=0, n_lo=300, n_hi=3000, radius_m=1410e3, max_cells=None):
         cen = cen[:max_cells]
     sizes = rng.integers(n_lo, n_hi + 1, len(cen))
     return make_cells(sizes, seed=seed + 1, centres=cen)
+
+
+class BinnedDay:
+    """Inputs of one reference day (GPR_CS2S3.py:200-221), synthetic:
+    ``sat`` (nx, ny, 4, T) binned freeboard of CS2 SAR, CS2 SARIN, S3A, S3B
+    (NaN = no observation; the slice ``obs[:, :, :, day:day+T]`` GPR:214),
+    ``sie`` (nx, ny) ice mask of the target day (NaN = no ice, GPR:213),
+    ``x``, ``y`` (nx, ny) grid coordinates [m], ``mean`` the prior (GPR:212)."""
+
+    def __init__(self, sat, sie, x, y, mean, date='20181205'):
+        self.sat, self.sie, self.x, self.y, self.mean, self.date = sat, sie, x, y, mean, date
+
+
+def make_binned_day(seed=0, nx=320, grid_m=GRID_M, ice_radius_m=1410e3, obs_radius_m=1700e3,
+                    cover=(0.02, 0.18), T=T_DAYS, nsat=4):
+    """A synthetic day on the 25 km polar grid: ice inside a disc of
+    ``ice_radius_m`` about the grid centre (~1e4 cells at 1410 km), satellite
+    coverage of each (cell, satellite, day) slot with probability varying
+    smoothly in ``cover`` (=> ~300-3000 observations within 300 km of a cell,
+    SURVEY §8d), freeboard field as ``cell_obs``."""
+    rng = np.random.default_rng(seed)
+    g = np.arange(nx, dtype=np.float64) * grid_m
+    x, y = np.meshgrid(g, g, indexing='ij')
+    c = g[nx // 2]
+    rr = np.sqrt((x - c) ** 2 + (y - c) ** 2)
+    sie = np.where(rr <= ice_radius_m, 0.9, np.nan)
+    p = cover[0] + (cover[1] - cover[0]) * 0.5 * (1 + np.sin(x / 7e5) * np.cos(y / 9e5))
+    p = np.where(rr <= obs_radius_m, p, 0.0)
+    sat = np.full((nx, nx, nsat, T), np.nan)
+    for d in range(T):
+        for s in range(nsat):
+            hit = rng.random((nx, nx)) < p
+            zf = (0.25 + 0.05 * np.sin(x / 2e5) * np.cos(y / 3e5) + 0.01 * d
+                  + 0.01 * s + rng.normal(0.0, 0.02, (nx, nx)))
+            sat[:, :, s, d] = np.where(hit, zf, np.nan)
+    return BinnedDay(sat, sie, x, y, PRIOR_MEAN)

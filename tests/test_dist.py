@@ -72,3 +72,38 @@ def test_partitions_cover_every_cell_once():
     parts = driver.lpt_partition(driver.cell_costs(sizes), 8)
     loads = [driver.cell_costs(sizes)[p].sum() for p in parts]
     assert max(loads) / min(loads) < 1.01
+
+
+def _allgather_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from optimalinterpolation_amd import day
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    ncell = 11
+    parts = day.split(np.arange(ncell), world)
+    mine = parts[rank]
+    rows = np.column_stack([mine * 10.0, mine + 0.5])
+    full = day._allgather_rows(rows, mine, ncell, device='cpu')
+    q.put((rank, full))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_day_allgather_every_rank_gets_all_rows():
+    """The day pipeline's single pass-1 exchange (day._allgather_rows): every
+    rank ends with the full ncell x m table (it then smooths locally)."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_allgather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = np.column_stack([np.arange(11) * 10.0, np.arange(11) + 0.5])
+    for _, full in got:
+        assert np.array_equal(full, ref)

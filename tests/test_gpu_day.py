@@ -1,0 +1,140 @@
+"""GPU parity of the day-level device steps against
+the CPU restatements in oracle/day_oracle.py, through the C ABI.
+
+  smoothing (GPR:65-76)        bit-exact vs the restatement (same window order,
+                               no FMA, numpy's nanmean summation order)
+  ball query (GPR:159)         exact index sets == scipy cKDTree (sorted)
+  gather (GPR:160-161)         bit-exact
+  day pipeline (GPR:200-336)   smoothed hyper fields bit-exact; pass-2 fields
+                               (interp_smth, interp_error_smth) within
+                               1e-10 * max(1, |ref|) (T1) of the oracle's
+                               GPR3D(opt=False) on the same smoothed hypers
+"""
+import numpy as np
+import pytest
+from scipy.spatial import cKDTree
+
+from oracle import day_oracle as D
+from optimalinterpolation_amd import _lib, day, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def same(a, b):
+    return np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize('std,shape', [(2, (320, 320)), (1, (70, 53)), (2, (17, 40))])
+def test_smooth_bit_exact(std, shape):
+    rng = np.random.default_rng(std + shape[0])
+    f = rng.normal(size=(5,) + shape) * np.array([1e5, 1e5, 3.0, 0.02, 0.01])[:, None, None]
+    f = np.abs(f) + np.array([2e5, 2e5, 1.0, 0.001, 0.0005])[:, None, None]
+    f[rng.random(f.shape) < 0.45] = np.nan
+    f[0, 3, 3] = np.inf
+    f[1, 5, 5] = -np.inf
+    f[2, 1:, 1:][rng.random(f[2, 1:, 1:].shape) < 0.05] = 50.0  # above vmax
+    f[3][:, :] = np.nan                                          # an all-NaN field
+    mask = np.where(rng.random(shape) < 0.8, 0.9, np.nan)
+    vmax = D.smooth_vmax(300, 9)
+    got = _lib.smooth_fields(f, vmax, mask, D.gaussian2d_kernel(std))
+    for k in range(5):
+        ref = D.smooth(f[k], vmax[k], mask, std)
+        assert same(got[k], ref), k
+
+
+def test_smooth_zero_replacement_bit_exact():
+    b = np.full((30, 30), np.nan)
+    b[15, 15] = 1.0
+    got = day.smooth(b, 5.0, np.ones((30, 30)), 1)
+    assert same(got, D.smooth(b, 5.0, np.ones((30, 30)), 1))
+
+
+def _day(seed=4, nx=64, ice=300e3, obs=700e3, cover=(0.02, 0.18)):
+    return synthetic.make_binned_day(seed=seed, nx=nx, ice_radius_m=ice, obs_radius_m=obs, cover=cover)
+
+
+def test_ball_query_equals_ckdtree():
+    d = _day()
+    xt, yt, tt, zt = D.training_set(d.sat, d.x, d.y)
+    pts = np.column_stack([xt, yt])
+    ids = np.where(~np.isnan(d.sie))
+    X = np.array([d.x[ids], d.y[ids]]).T
+    offs, idx = _lib.ball_query(pts, X, 300e3)
+    tree = cKDTree(pts)
+    assert offs[0] == 0 and len(idx) == offs[-1]
+    for c in range(len(X)):
+        ref = np.sort(np.asarray(tree.query_ball_point(x=X[c], r=300e3), dtype=np.int64))
+        assert np.array_equal(idx[offs[c]:offs[c + 1]], ref), c
+    # gather of those rows, bit-exact
+    xyt, zz = _lib.gather_rows(xt, yt, tt, zt, idx)
+    assert np.array_equal(xyt, np.stack([xt[idx], yt[idx], tt[idx]], axis=1))
+    assert np.array_equal(zz, zt[idx])
+
+
+def test_ball_query_edges():
+    pts = np.array([[0.0, 0.0], [180e3, 240e3], [300e3, 0.0], [300e3 + 1e-6, 0.0], [-300e3, 0.0]])
+    offs, idx = _lib.ball_query(pts, np.array([[0.0, 0.0], [5e6, 5e6]]), 300e3)
+    assert list(offs) == [0, 4, 4] and list(idx) == [0, 1, 2, 4]
+    offs, idx = _lib.ball_query(np.zeros((0, 2)), np.array([[0.0, 0.0]]), 300e3)
+    assert list(offs) == [0, 0] and len(idx) == 0
+    # more than one chunk of 256 with hits spread over chunks, ascending order
+    rng = np.random.default_rng(0)
+    p = rng.uniform(-1e6, 1e6, (5000, 2))
+    offs, idx = _lib.ball_query(p, np.array([[0.0, 0.0], [9e5, -9e5]]), 3e5)
+    for c, q in enumerate([[0.0, 0.0], [9e5, -9e5]]):
+        assert np.array_equal(idx[offs[c]:offs[c + 1]], D.ball_query(p, np.array(q), 3e5))
+
+
+def test_gather_rejects_bad_index():
+    with pytest.raises(_lib.OiError):
+        _lib.gather_rows(np.zeros(3), np.zeros(3), np.zeros(3), np.zeros(3), np.array([0, 3]))
+
+
+def _pass1_rows(d):
+    """Plausible pass-1 fields without running the optimiser: hypers varying
+    smoothly in space, a few failed (NaN) and out-of-range cells."""
+    ids = np.where(~np.isnan(d.sie))
+    X = np.array([d.x[ids], d.y[ids]]).T
+    u = np.sin(X[:, 0] / 3e5) * np.cos(X[:, 1] / 4e5)
+    rows = np.column_stack([0.3 + 0.01 * u, 0.02 + 0.001 * u, -100 + u, 2.5e5 * (1.1 + u),
+                            3.0e5 * (1.1 - 0.5 * u), 6.0 + 2 * u, 4e-3 * (1.2 + u),
+                            8e-4 * (1.2 - 0.5 * u)])
+    rows[3] = np.nan          # a non-PD cell (GPR:187-191)
+    rows[5, 3] = 2e6          # above vmax = 600 km (GPR:303)
+    return rows
+
+
+@pytest.mark.parametrize('neighbours', ['device', 'kdtree'])
+def test_day_pass2_matches_oracle(neighbours):
+    d = _day(seed=7, nx=48, ice=200e3, obs=500e3, cover=(0.02, 0.06))
+    rows = _pass1_rows(d)
+    res = day.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='20181205', neighbours=neighbours,
+                              pass1_rows=rows)
+    ref = D.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='20181205', pass1_rows=rows)
+    assert set(res) == set(ref)
+    for k in day.PASS1_KEYS:
+        assert same(res['20181205_' + k], ref['20181205_' + k]), k
+    for k in day.HYPER_KEYS:
+        assert same(res['20181205_' + k + '_smth'], ref['20181205_' + k + '_smth']), k
+    for k in ('interp_smth', 'interp_error_smth'):
+        a, b = res['20181205_' + k], ref['20181205_' + k]
+        assert np.array_equal(np.isnan(a), np.isnan(b)), k
+        ok = ~np.isnan(b)
+        assert np.all(np.abs(a[ok] - b[ok]) <= 1e-10 * np.maximum(1.0, np.abs(b[ok]))), k
+
+
+def test_day_full_fit_runs_and_is_consistent():
+    """opt=True end to end on a small day: every ice cell has finite fields, the
+    pass-1 fields feed the smoothing exactly as the oracle would smooth them,
+    and pass 2 equals the oracle's GPR3D(opt=False) on those smoothed hypers."""
+    d = _day(seed=8, nx=40, ice=120e3, obs=450e3, cover=(0.02, 0.05))
+    res = day.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='d')
+    ids = np.where(~np.isnan(d.sie))
+    assert np.isfinite(res['d_interp'][ids]).all() and np.isfinite(res['d_interp_smth'][ids]).all()
+    rows = np.column_stack([res['d_' + k][ids] for k in day.PASS1_KEYS])
+    ref = D.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='d', pass1_rows=rows)
+    for k in day.HYPER_KEYS:
+        assert same(res['d_' + k + '_smth'], ref['d_' + k + '_smth']), k
+    a, b = res['d_interp_smth'][ids], ref['d_interp_smth'][ids]
+    assert np.all(np.abs(a - b) <= 1e-10 * np.maximum(1.0, np.abs(b)))
+    assert res.info['evals'][~np.isnan(res.info['evals'])].min() >= 1
