@@ -21,7 +21,13 @@ pytestmark = pytest.mark.gpu
 
 
 def same(a, b):
-    return np.array_equal(a, b, equal_nan=True)
+    ok = np.array_equal(a, b, equal_nan=True)
+    if not ok:  # diagnostics for the failure message
+        bad = ~((a == b) | (np.isnan(a) & np.isnan(b)))
+        d = np.abs(a - b)[bad]
+        print(f"mismatch: {bad.sum()} entries, max |d| {np.nanmax(d) if d.size else 0}, "
+              f"nan-pattern equal {np.array_equal(np.isnan(a), np.isnan(b))}")
+    return ok
 
 
 @pytest.mark.parametrize('std,shape', [(2, (320, 320)), (1, (70, 53)), (2, (17, 40))])
