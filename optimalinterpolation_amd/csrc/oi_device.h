@@ -58,8 +58,11 @@ extern "C" {
 // `list` holds indices into `cells` sorted by T descending.
 int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
-int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
+int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j, int kbeg,
+                    void* stream);
 int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
+                         int kbeg, int with_trtri, void* stream);
+int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
                          int with_trtri, void* stream);
 int oi_launch_zvec(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);

@@ -116,9 +116,21 @@ size_t cell_bytes(int64_t n, bool eval) {
 }
 
 // ------------------------------------------------------------- profiling
-enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_ZVEC, K_AVEC, K_LAUUM, K_FINAL, K_PRED, K_COUNT };
-const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_chol_panel", "k_zvec",
-                                    "k_avec",  "k_lauum_grad",  "k_finalize", "k_predict"};
+enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_EVEN, K_ZVEC, K_AVEC, K_LAUUM, K_FINAL, K_PRED, K_COUNT };
+const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_chol_panel",
+                                    "k_panel_even", "k_zvec", "k_avec", "k_lauum_grad",
+                                    "k_finalize", "k_predict"};
+
+// Panel scheme, read per call from OI_PANEL:
+//   1 (default): one-column left-looking panels, every column streams its
+//                whole block row of L (and of W = L^-1);
+//   2          : even/odd column pairs share one stream (k_panel_even +
+//                k_chol_panel(kbeg = j-1)): half the L / W traffic, measured
+//                equal in time on the day workload (round 1).
+bool legacy_panels() {
+  const char* e = getenv("OI_PANEL");
+  return !(e && atoi(e) == 2);
+}
 struct KStat {
   int64_t launches = 0;
   double ms = 0.0;
@@ -283,6 +295,7 @@ int run(const Job& job, const oi_options& o) {
       throw HipError("residual kernel launch failed");
   }
   const bool eval_mem = job.kind != Job::PREDICT_ONLY;
+  const bool legacy = legacy_panels();
 
   // admission order: largest cells first (cost ~ n^3), ties by index
   std::vector<int64_t> order(ncell);
@@ -493,20 +506,37 @@ int run(const Job& job, const oi_options& o) {
       mark(K_CHOL, false);
       rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, gst);
       mark(K_CHOL, true);
+      const bool even = !legacy && (j % 2 == 0);
+      const int kbeg = (legacy || even) ? 0 : j - 1;
       mark(K_SCALE, false);
-      rc |= oi_launch_scale(dc, dl_all, cnt, j, gst);
+      rc |= oi_launch_scale(dc, dl_all, cnt, j, kbeg, gst);
       mark(K_SCALE, true);
-      mark(K_TRSM, false);
-      rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
-      mark(K_TRSM, true);
+      if (even) {
+        mark(K_EVEN, false);
+        rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
+        mark(K_EVEN, true);
+      } else {
+        mark(K_TRSM, false);
+        rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, gst);
+        mark(K_TRSM, true);
+      }
       if (o.profile) {  // executed MFMA flops: 2*64^3 per 64x64 tile product
         for (int k = 0; k < cnt; ++k) {
           const OiCell& cd = hc[all_slots[k]];
-          kfl[K_SCALE] += tf * (double)j;
-          kfl[K_TRSM] += tf * (double)(cd.T - 1 - j) * (j + 1);
-          if (cd.T - 1 - j > 0) kfl[K_TRSM] += tf * (double)(j + 1);  // look-ahead diagonal
-          if (cd.mode == OI_MODE_EVAL)
-            for (int jj = 0; jj < j; ++jj) kfl[K_TRSM] += tf * (double)(j - jj);
+          const bool ev = cd.mode == OI_MODE_EVAL;
+          kfl[K_SCALE] += tf * (double)(j - kbeg);
+          if (even) {  // 64x128 blocks: two products per streamed pair
+            kfl[K_EVEN] += tf * 2.0 * (double)(cd.T - 1 - j) * (j + 1);
+            if (cd.T - 1 - j > 0) kfl[K_EVEN] += tf;  // fresh look-ahead product
+            if (ev)
+              for (int jj = 0; jj < j; ++jj) kfl[K_EVEN] += tf * 2.0 * (double)(j - jj);
+          } else {
+            kfl[K_TRSM] += tf * (double)(cd.T - 1 - j) * (j + 1 - kbeg);
+            if (cd.T - 1 - j > 0) kfl[K_TRSM] += tf * (double)(j + 1);  // look-ahead diagonal
+            if (ev)
+              for (int jj = 0; jj < j; ++jj)
+                kfl[K_TRSM] += tf * (double)(j - std::max(jj, kbeg) + (kbeg > jj ? 1 : 0));
+          }
         }
       }
     }

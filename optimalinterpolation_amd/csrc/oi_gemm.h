@@ -48,45 +48,48 @@ __device__ __forceinline__ int acc_col(int nb) {
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0)
 
 // pair(p, a, b0, b1): the p-th operand triple (A tile, B tile of the left
-// half, B tile of the right half).  Register staging, two LDS buffers.
+// half, B tile of the right half).  Register staging is a two-deep ring
+// (chunks ch+1 and ch+2 in flight while ch is multiplied out of LDS), two LDS
+// buffers; threads 0..255 stage A and B0, threads 256..511 stage B1.
+typedef double dv2 __attribute__((ext_vector_type(2)));
+struct StageRegs {
+  dv2 a0, a1, b0, b1;
+};
+
 template <class PairFn>
 __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = (w >> 2) & 1, wc = w & 3;
-  const int nch = npairs * (GNB / KC);
+  const int nch = npairs * (GNB / KC);  // even
   if (nch == 0) return;
   const int tt = t & 255, half = t >> 8;
   const int sk = tt >> 4, sm = (tt & 15) * 4;
-  double2 ra0, ra1, rb0, rb1;
-  auto load = [&](int ch) {
+  const int fr = lane & 15, fk = lane >> 4;
+  StageRegs r0, r1;
+  auto load = [&](int ch, StageRegs& q) __attribute__((always_inline)) {
     const double *pa, *pb0, *pb1;
     pair(ch >> 2, pa, pb0, pb1);
     const int off = (ch & 3) * KC * GNB + tt * 4;
     if (half == 0) {
-      ra0 = *(const double2*)(pa + off);
-      ra1 = *(const double2*)(pa + off + 2);
+      q.a0 = *(const dv2*)(pa + off);
+      q.a1 = *(const dv2*)(pa + off + 2);
     }
     const double* pb = half ? pb1 : pb0;
-    rb0 = *(const double2*)(pb + off);
-    rb1 = *(const double2*)(pb + off + 2);
+    q.b0 = *(const dv2*)(pb + off);
+    q.b1 = *(const dv2*)(pb + off + 2);
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const StageRegs& q) __attribute__((always_inline)) {
     double* As = lds + buf * (STAGE_A + STAGE_B);
     double* Bs = As + STAGE_A;
     if (half == 0) {
-      *(double2*)(As + sk * LDSA + sm) = ra0;
-      *(double2*)(As + sk * LDSA + sm + 2) = ra1;
+      *(dv2*)(As + sk * LDSA + sm) = q.a0;
+      *(dv2*)(As + sk * LDSA + sm + 2) = q.a1;
     }
-    *(double2*)(Bs + sk * LDSB + 64 * half + sm) = rb0;
-    *(double2*)(Bs + sk * LDSB + 64 * half + sm + 2) = rb1;
+    *(dv2*)(Bs + sk * LDSB + 64 * half + sm) = q.b0;
+    *(dv2*)(Bs + sk * LDSB + 64 * half + sm + 2) = q.b1;
   };
-  load(0);
-  store(0);
-  __syncthreads();
-  const int fr = lane & 15, fk = lane >> 4;
-  for (int ch = 0; ch < nch; ++ch) {
-    if (ch + 1 < nch) load(ch + 1);
-    const double* As = lds + (ch & 1) * (STAGE_A + STAGE_B);
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const double* As = lds + buf * (STAGE_A + STAGE_B);
     const double* Bs = As + STAGE_A;
 #pragma unroll
     for (int kk = 0; kk < KC / 4; ++kk) {
@@ -100,7 +103,19 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
       acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
       acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
     }
-    if (ch + 1 < nch) store((ch + 1) & 1);
+  };
+  load(0, r0);
+  load(1, r1);
+  store(0, r0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ch += 2) {
+    if (ch + 2 < nch) load(ch + 2, r0);
+    compute(0);
+    store(1, r1);
+    __syncthreads();
+    if (ch + 3 < nch) load(ch + 3, r1);
+    compute(1);
+    if (ch + 2 < nch) store(0, r0);
     __syncthreads();
   }
 }
@@ -145,11 +160,6 @@ __device__ __forceinline__ int acc1_col(int nb) {
 // ch is multiplied out of LDS): 66 TF/s vs 57 TF/s for a one-deep prefetch
 // when one operand is L2-resident (tools/gemm_probe3.hip).  Native vector
 // types (not HIP's double2 struct) keep the ring in VGPRs.
-typedef double dv2 __attribute__((ext_vector_type(2)));
-struct StageRegs {
-  dv2 a0, a1, b0, b1;
-};
-
 template <class PairFn>
 __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;

@@ -227,13 +227,13 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
 // D = P^T = -L_jk^T Dinv_jj^T is stored coalesced as P[n][m].
 #define SCALE_KPW 4
 __global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
-                                               const int32_t* __restrict__ list, int j, int gx,
-                                               int ncell) {
+                                               const int32_t* __restrict__ list, int j, int kbeg,
+                                               int gx, int ncell) {
   __shared__ __attribute__((aligned(16))) double As[NB * LDSA];  // As[q][m] = L_jk[q][m]
   int ci, g;
   if (!xcd_cell_slot(gx, ncell, ci, g)) return;
   const OiCell& c = cells[list[ci]];
-  const int k0 = g * SCALE_KPW;
+  const int k0 = kbeg + g * SCALE_KPW;
   if (j >= c.T || k0 >= j || *c.status != OI_OK) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
   const int fr = lane & 15, fk = lane >> 4;
@@ -290,8 +290,8 @@ __global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
 //   x >= T-1-j : (eval) tile (j, jj = x-(T-1-j)) of W = L^-1:
 //                  W_j,jj = sum_{k=jj}^{j-1} P_jk W_k,jj
 __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ cells,
-                                                   const int32_t* __restrict__ list, int j, int gx,
-                                                   int ncell) {
+                                                   const int32_t* __restrict__ list, int j,
+                                                   int kbeg, int gx, int ncell) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
   int ci, x;
   if (!xcd_cell_slot(gx, ncell, ci, x)) return;
@@ -305,9 +305,10 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   quad_zero(acc);
   if (x < ntrsm) {
     const int i = j + 1 + x;
-    gemm1_kmajor(acc, lds, j + 1, [&](int p, const double*& a, const double*& b) {
-      a = p < j ? Pj + (size_t)p * OI_TILE : Dj;
-      b = tileL(c, i, p);
+    gemm1_kmajor(acc, lds, j + 1 - kbeg, [&](int p, const double*& a, const double*& b) {
+      const int k = kbeg + p;
+      a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
+      b = tileL(c, i, k);  // k == j: A_ij, already holding A_ij - sum_{k<kbeg} L_ik L_jk^T
     });
     double* Y = tileL(c, i, j);
     for (int mb = 0; mb < 2; ++mb)
@@ -356,16 +357,132 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   }
   const int jj = x - ntrsm;
   if (c.mode != OI_MODE_EVAL || jj >= j) return;
-  gemm1_kmajor(acc, lds, j - jj, [&](int p, const double*& a, const double*& b) {
-    const int k = jj + p;
-    a = Pj + (size_t)k * OI_TILE;
-    b = tileW(c, k, jj);
+  // kbeg > jj: W_j,jj holds Vneg = -sum_{k=jj}^{kbeg-1} L_jk W_k,jj (k_panel_even), so
+  // W_j,jj = sum_{k=kbeg}^{j-1} P_jk W_k,jj + Dinv_jj Vneg
+  const int kfirst = jj > kbeg ? jj : kbeg, extra = kbeg > jj ? 1 : 0;
+  gemm1_kmajor(acc, lds, j - kfirst + extra, [&](int p, const double*& a, const double*& b) {
+    const int k = kfirst + p;
+    a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
+    b = tileW(c, k, jj);  // k == j: Vneg
   });
   double* Wt = tileW(c, j, jj);
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
       for (int r = 0; r < 4; ++r)
         Wt[acc1_row(mb, r) * NB + acc1_col(nb)] = acc.c[mb][nb][r];  // row-major
+}
+
+// --------------------------------------------------- k_panel_even(j), j even
+// Shared-stream form of two consecutive block columns: every streamed tile
+// feeds two outputs (64 x 128 block per 512-thread workgroup, gemm2 core), so
+// the L / W streams of the left-looking factorisation are read from HBM once
+// per PAIR of columns.  Slots of a cell:
+//   x <  T-1-j : row i = j+1+x of the factor:
+//                  L_ij      = sum_{k<j} L_ik P_jk^T + A_ij Dinv_jj^T
+//                  A_i,j+1  -= sum_{k<j} L_ik L_j+1,k^T     (partial update of
+//                              column j+1; k_chol_panel(j+1, kbeg=j) adds k = j)
+//                i = j+1 (x = 0) instead completes A_j+1,j+1 (look-ahead):
+//                  A_j+1,j+1 -= sum_{k<j} L_j+1,k L_j+1,k^T + L_j+1,j L_j+1,j^T
+//   x >= T-1-j : (eval) jj = x-(T-1-j) < j, rows j and j+1 of W = L^-1:
+//                  W_j,jj    = sum_{k=jj}^{j-1} P_jk W_k,jj
+//                  W_j+1,jj  = Vneg := -sum_{k=jj}^{j-1} L_j+1,k W_k,jj  (finished
+//                              by k_chol_panel(j+1, kbeg=j))
+// Accumulators come out transposed with respect to the tile storage, so each
+// 64x64 half goes through LDS and is written back with coalesced 16 B rows.
+#define XLD 65  // LDS row stride of a staged 64x64 tile (doubles)
+enum { EMIT_STORE = 0, EMIT_SUB = 1, EMIT_NEG = 2 };
+
+// dst[n*64 + m] (op)= D_h[m][n] for the 64x64 half h of a gemm2 accumulator.
+// Leaves the staged tile in X[n*XLD + m] (= dst's storage order) for reuse.
+__device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, double* dst, int op) {
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if (((w & 3) >> 1) == h) {
+    for (int mb = 0; mb < 2; ++mb)
+      for (int nb = 0; nb < 2; ++nb)
+        for (int r = 0; r < 4; ++r)
+          X[(acc_col(nb) - 64 * h) * XLD + acc_row(mb, r)] = acc.c[mb][nb][r];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < OI_TILE; e += GEMM_THREADS) {
+    const double v = X[(e >> 6) * XLD + (e & 63)];
+    if (op == EMIT_STORE)
+      dst[e] = v;
+    else if (op == EMIT_SUB)
+      dst[e] = dst[e] - v;
+    else
+      dst[e] = -v;
+  }
+}
+
+__global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __restrict__ cells,
+                                                            const int32_t* __restrict__ list,
+                                                            int j, int gx, int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
+  static_assert(NB * XLD <= GEMM2_LDS, "staging tile must fit the GEMM LDS");
+  int ci, x;
+  if (!xcd_cell_slot(gx, ncell, ci, x)) return;
+  const OiCell& c = cells[list[ci]];
+  const int T = c.T;
+  if (j >= T || *c.status != OI_OK) return;
+  const int ntrsm = T - 1 - j;
+  const bool has_next = j + 1 < T;
+  const double* Pj = c.P;
+  const double* Dj = tileD(c, j);
+  Quad acc;
+  quad_zero(acc);
+  if (x < ntrsm) {
+    const int i = j + 1 + x;
+    gemm2_kmajor(acc, lds, j + 1,
+                 [&](int p, const double*& a, const double*& b0, const double*& b1) {
+                   if (p < j) {
+                     a = tileL(c, i, p);
+                     b0 = Pj + (size_t)p * OI_TILE;
+                     b1 = tileL(c, j + 1, p);
+                   } else {
+                     a = tileL(c, i, j);  // A_ij
+                     b0 = Dj;
+                     b1 = g_zero_tile;
+                   }
+                 });
+    emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij
+    if (x != 0) {
+      emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1
+      return;
+    }
+    // i = j+1: add the fresh L_j+1,j L_j+1,j^T (staged in lds as X[q*XLD + m] =
+    // L[m][q]) to the half-1 accumulator, then complete A_j+1,j+1.
+    __syncthreads();
+    {
+      const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+      const int wr = (w >> 2) & 1, wc = w & 3, fr = lane & 15, fk = lane >> 4;
+      if ((wc >> 1) == 1) {
+        const int c0 = 32 * (wc - 2);
+#pragma unroll 4
+        for (int kk = 0; kk < NB / 4; ++kk) {
+          const int q = kk * 4 + fk;
+          const double a0 = lds[q * XLD + 32 * wr + fr], a1 = lds[q * XLD + 32 * wr + 16 + fr];
+          const double b0 = lds[q * XLD + c0 + fr], b1 = lds[q * XLD + c0 + 16 + fr];
+          acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+          acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+          acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+          acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+        }
+      }
+    }
+    emit_half(acc, 1, lds, tileL(c, i, i), EMIT_SUB);
+    return;
+  }
+  const int jj = x - ntrsm;
+  if (c.mode != OI_MODE_EVAL || jj >= j) return;
+  gemm2_kmajor(acc, lds, j - jj, [&](int p, const double*& a, const double*& b0, const double*& b1) {
+    const int k = jj + p;
+    a = tileW(c, k, jj);
+    b0 = Pj + (size_t)k * OI_TILE;
+    b1 = has_next ? tileL(c, j + 1, k) : g_zero_tile;
+  });
+  emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);           // W_j,jj (row-major)
+  if (has_next) emit_half(acc, 1, lds, tileW(c, j + 1, jj), EMIT_NEG);  // Vneg
 }
 
 // ------------------------------------------------------------- k_zvec
@@ -764,20 +881,29 @@ extern "C" int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, i
 }
 
 extern "C" int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j,
-                               void* stream) {
-  if (ncell <= 0 || j <= 0) return 0;
-  const int gx = (j + SCALE_KPW - 1) / SCALE_KPW;
-  hipLaunchKernelGGL(k_scale, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, gx,
-                     ncell);
+                               int kbeg, void* stream) {
+  if (ncell <= 0 || j - kbeg <= 0) return 0;
+  const int gx = (j - kbeg + SCALE_KPW - 1) / SCALE_KPW;
+  hipLaunchKernelGGL(k_scale, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j,
+                     kbeg, gx, ncell);
   return ret();
 }
 
 extern "C" int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                                    int j, int with_trtri, void* stream) {
+                                    int j, int kbeg, int with_trtri, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
   hipLaunchKernelGGL(k_chol_panel, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j,
-                     gx, ncell);
+                     kbeg, gx, ncell);
+  return ret();
+}
+
+extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT,
+                                    int j, int with_trtri, void* stream) {
+  const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
+  if (ncell <= 0 || gx <= 0) return 0;
+  hipLaunchKernelGGL(k_panel_even, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
+                     list, j, gx, ncell);
   return ret();
 }
 

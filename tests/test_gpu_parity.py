@@ -157,3 +157,30 @@ def test_gpr3d_n0_edge():
     assert np.array_equal(out[0], np.array(ref, float))
     assert np.signbit(out[0, 2])
     assert info[0, 1] == 0 and info[0, 3] == 1
+
+
+@pytest.mark.parametrize('scheme', ['1', '2'])
+def test_panel_schemes_agree(scheme, monkeypatch):
+    """Both Cholesky panel schemes (OI_PANEL=1 one column per launch, =2 paired
+    columns sharing one stream) meet the T1 tolerance on tile-boundary sizes."""
+    monkeypatch.setenv('OI_PANEL', scheme)
+    sizes = [63, 64, 65, 129, 200, 257, 700]
+    cells = synthetic.make_cells(sizes, seed=11)
+    h = np.tile(np.array([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(1e-3), 0.]),
+                (len(sizes), 1))
+    mX = np.full(len(cells.z), cells.mean)
+    nlz, grad, st = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, h)
+    for c in range(len(sizes)):
+        x, y, _ = cells.cell(c)
+        f, g = O.neg_log_ml(h[c], x, y, np.full(len(y), cells.mean))
+        f = float(np.asarray(f).item())
+        assert abs(nlz[c] - f) <= RTOL * max(1.0, abs(f)), (scheme, sizes[c])
+        S = grad_scale(h[c], x, y, np.full(len(y), cells.mean))
+        assert np.all(np.abs(grad[c] - g) <= RTOL * (np.abs(g) + S)), (scheme, sizes[c])
+    hyp = np.tile(synthetic.FIXED_HYPERS, (len(sizes), 1))
+    out, st2, _ = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+    for c in range(len(sizes)):
+        x, y, xs = cells.cell(c)
+        fs, sd, lZ = O.predict(x, y, xs, cells.mean, hyp[c, :3], hyp[c, 3], hyp[c, 4])
+        assert abs(out[c, 0] - fs[0]) <= RTOL * max(1, abs(fs[0]))
+        assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
