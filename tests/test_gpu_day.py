@@ -144,3 +144,20 @@ def test_day_full_fit_runs_and_is_consistent():
     a, b = res['d_interp_smth'][ids], ref['d_interp_smth'][ids]
     assert np.all(np.abs(a - b) <= 1e-10 * np.maximum(1.0, np.abs(b)))
     assert res.info['evals'][~np.isnan(res.info['evals'])].min() >= 1
+
+
+def test_day_12p5km_grid_pass2():
+    """The 12.5 km configuration (BASELINE config 5): smoothing width std=1
+    (GPR:298-302), a 640-wide grid, pass 2 against the oracle."""
+    d = synthetic.make_binned_day(seed=9, nx=640, grid_m=12.5e3, ice_radius_m=150e3,
+                                  obs_radius_m=460e3, cover=(0.004, 0.012))
+    rows = _pass1_rows(d)
+    res = day.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='d', grid_res=12.5,
+                              pass1_rows=rows)
+    ref = D.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='d', grid_res=12.5,
+                            pass1_rows=rows)
+    for k in day.HYPER_KEYS:
+        assert same(res['d_' + k + '_smth'], ref['d_' + k + '_smth']), k
+    ids = np.where(~np.isnan(d.sie))
+    a, b = res['d_interp_smth'][ids], ref['d_interp_smth'][ids]
+    assert np.all(np.abs(a - b) <= 1e-10 * np.maximum(1.0, np.abs(b)))

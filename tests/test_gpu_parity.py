@@ -184,3 +184,28 @@ def test_panel_schemes_agree(scheme, monkeypatch):
         fs, sd, lZ = O.predict(x, y, xs, cells.mean, hyp[c, :3], hyp[c, 3], hyp[c, 4])
         assert abs(out[c, 0] - fs[0]) <= RTOL * max(1, abs(fs[0]))
         assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
+
+
+def test_config5_size_n5000():
+    """BASELINE config 5 allows n up to 5000 per cell (T = 79 tiles): SMLII and
+    the predict block at that size, T1 tolerance, one cell each."""
+    n = 5000
+    cells = synthetic.make_cells([n], seed=5000)
+    h = np.array([[np.log(2.2e5), np.log(1.8e5), np.log(6.), np.log(5e-3), np.log(1e-3), 0.0]])
+    mX = np.full(n, cells.mean)
+    nlz, grad, status = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, h)
+    x, y, xs = cells.cell(0)
+    f, g = O.neg_log_ml(h[0], x, y, mX)
+    f = float(np.asarray(f).item())
+    assert status[0] == 0
+    ok, err = close(nlz[0], f)
+    assert ok, (nlz[0], f, err)
+    sc = np.abs(g) + grad_scale(h[0], x, y, mX)
+    ok, err = close(grad[0], g, scale=np.maximum(sc, 1e-300))
+    assert ok, (grad[0], g, err)
+    hyp = np.exp(h[:, :5])
+    out, st, _ = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+    fs, sd, lZ = O.predict(x, y, xs, cells.mean, hyp[0, :3], hyp[0, 3], hyp[0, 4])
+    for got, ref in ((out[0, 0], fs[0]), (out[0, 1], sd[0])):
+        ok, err = close(got, ref)
+        assert ok, (got, ref, err)
