@@ -20,7 +20,8 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'liboi.so')
+# OI_LIB: load a differently-built variant (A/B experiments); default the in-tree build
+LIB_PATH = os.environ.get('OI_LIB') or os.path.join(_HERE, 'liboi.so')
 
 _lib = None
 _lock = threading.Lock()

@@ -71,6 +71,7 @@ int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, in
 int oi_launch_predict(const OiCell* cells, const int32_t* list, int ncell, void* stream);
 int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, void* stream);
 // r[a] = y[a] - (mX ? mX[a] : 1.0 * mean)
+int oi_set_debug(int on);
 int oi_launch_residual(const double* y, const double* mX, double mean, double* r, int64_t N,
                        void* stream);
 #ifdef __cplusplus

@@ -296,6 +296,16 @@ int run(const Job& job, const oi_options& o) {
   }
   const bool eval_mem = job.kind != Job::PREDICT_ONLY;
   const bool legacy = legacy_panels();
+  static const bool debug_set = [] {
+    const char* e = getenv("OI_DEBUG");
+    if (e && atoi(e) == 1) oi_set_debug(1);
+    return true;
+  }();
+  (void)debug_set;
+  const bool poison = [] {
+    const char* e = getenv("OI_POISON");
+    return e && atoi(e) == 1;
+  }();
 
   // admission order: largest cells first (cost ~ n^3), ties by index
   std::vector<int64_t> order(ncell);
@@ -387,6 +397,8 @@ int run(const Job& job, const oi_options& o) {
       sl.cell = c;
       sl.off = off;
       sl.bytes = bytes;
+      if (poison)  // debug: NaN-fill the cell's workspace so any read-before-write shows
+        HIPC(hipMemsetAsync(ctx.arena.ptr(off), 0xFF, bytes, gr.st));
       OiCell& cd = hc[s];
       std::memset(&cd, 0, sizeof(cd));
       const int T = tiles_of(n);

@@ -30,6 +30,9 @@
 #include "oi_device.h"
 #include "oi_gemm.h"
 
+// GEMM1(acc, lds, npairs, pair): the 64x64 tile-GEMM loop of the panel / lauum kernels
+#define GEMM1(acc, lds, np, fn) gemm1_kmajor(acc, lds, np, fn)
+
 #define NB OI_NB
 #define SQRT3 1.7320508075688772
 #define LOG2PI 1.8378770664093453  // np.log(2*np.pi)
@@ -37,6 +40,12 @@
 // structurally-zero operand tile (tiles above the block diagonal); device
 // globals are zero-initialised by the loader and never written
 __device__ double g_zero_tile[OI_TILE];
+// OI_DEBUG=1 (oi_set_debug): diagnostic printf from the factorisation
+__device__ int g_debug;
+
+extern "C" int oi_set_debug(int on) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_debug), &on, sizeof(int)) == hipSuccess ? 0 : -1;
+}
 
 __device__ __forceinline__ size_t tri(int i) { return (size_t)i * (i + 1) / 2; }
 __device__ __forceinline__ double* tileL(const OiCell& c, int i, int j) {
@@ -182,7 +191,12 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
     for (int s2 = cc + 1; s2 < NB; ++s2) R[s2] -= lr * rdlane(R[cc], s2);
   }
   if (!ok) {
-    if (r == 0) *c.status = OI_NOT_PD;
+    if (r == 0) {
+      *c.status = OI_NOT_PD;
+      if (g_debug)
+        printf("oi debug: not PD: cell n=%d T=%d diagonal tile j=%d hyp %g %g %g %g %g\n", c.n, c.T,
+               j, c.hyp[0], c.hyp[1], c.hyp[2], c.hyp[3], c.hyp[4]);
+    }
     return;
   }
   double lg = 0.0;
@@ -305,7 +319,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   quad_zero(acc);
   if (x < ntrsm) {
     const int i = j + 1 + x;
-    gemm1_kmajor(acc, lds, j + 1 - kbeg, [&](int p, const double*& a, const double*& b) {
+    GEMM1(acc, lds, j + 1 - kbeg, [&](int p, const double*& a, const double*& b) {
       const int k = kbeg + p;
       a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
       b = tileL(c, i, k);  // k == j: A_ij, already holding A_ij - sum_{k<kbeg} L_ik L_jk^T
@@ -342,7 +356,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       }
     }
     __syncthreads();
-    gemm1_kmajor(accd, lds, j, [&](int p, const double*& a, const double*& b) {
+    GEMM1(accd, lds, j, [&](int p, const double*& a, const double*& b) {
       a = tileL(c, i, p);
       b = a;
     });
@@ -360,7 +374,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   // kbeg > jj: W_j,jj holds Vneg = -sum_{k=jj}^{kbeg-1} L_jk W_k,jj (k_panel_even), so
   // W_j,jj = sum_{k=kbeg}^{j-1} P_jk W_k,jj + Dinv_jj Vneg
   const int kfirst = jj > kbeg ? jj : kbeg, extra = kbeg > jj ? 1 : 0;
-  gemm1_kmajor(acc, lds, j - kfirst + extra, [&](int p, const double*& a, const double*& b) {
+  GEMM1(acc, lds, j - kfirst + extra, [&](int p, const double*& a, const double*& b) {
     const int k = kfirst + p;
     a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
     b = tileW(c, k, jj);  // k == j: Vneg
@@ -644,7 +658,7 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
   if (*c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
   Quad acc;
   quad_zero(acc);
-  gemm1_kmajor(acc, lds, T - i, [&](int p, const double*& a, const double*& b) {
+  GEMM1(acc, lds, T - i, [&](int p, const double*& a, const double*& b) {
     a = tileW(c, i + p, i);
     b = tileW(c, i + p, j);
   });
