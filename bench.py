@@ -2,8 +2,9 @@
 opt=True) on the synthetic 25 km pan-Arctic day, fp64 (BASELINE.json).
 
 A *step* is one shard of the day: the ~1e4 cells of the day (n ~ U{300..3000}
-observations each) are dealt by a seeded shuffle into
-8 shards of equal size; step s on rank r processes shard (s*N + r) mod 8.  So
+observations each) are dealt into 8 shards of equal
+estimated cost (LPT on E(n)*n^3, driver.cell_costs); step s on rank r
+processes shard (s*N + r) mod 8.  So
 `--gpus 8 --steps 1` is exactly one whole day sharded over 8 GPUs (config 4)
 with the final RCCL gather of the posterior fields to rank 0, and
 `--gpus 1 --steps 2` times a quarter of the day on one GPU.
@@ -49,9 +50,11 @@ def parse():
 def build_steps(args, rank, world):
     from optimalinterpolation_amd import synthetic
     if args.workload == 'day':
+        from optimalinterpolation_amd import driver
         day = synthetic.make_day(seed=args.seed)
-        perm = np.random.default_rng(args.seed + 99).permutation(day.ncell)
-        shards = [np.sort(perm[s::NSHARDS]) for s in range(NSHARDS)]
+        # equal-cost shards: LPT on the n^3 * E(n) cost model (driver.cell_costs),
+        # so every rank of a weak-scaling run gets the same amount of work
+        shards = driver.lpt_partition(driver.cell_costs(day.sizes), NSHARDS)
         steps = []
         for g in range(args.warmup + args.steps):
             steps.append(day.subset(shards[(g * world + rank) % NSHARDS]))
