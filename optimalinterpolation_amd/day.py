@@ -203,7 +203,10 @@ def interpolate_day(sat, sie, x, y, mean, date='', T=9, radius=300, grid_res=25,
         x0 = [np.log(grid_res * 1000), np.log(grid_res * 1000), np.log(1.), np.log(1.), np.log(1.),
               np.log(.1)]
     x0 = np.asarray(x0, dtype=np.float64)
-    dev = torch.device('cuda', device)
+    # ``device``: GPU ordinal (the product); a torch device string such as
+    # 'cpu' is accepted only so the multi-rank plumbing can be tested without
+    # a GPU (tests substitute the liboi calls)
+    dev = torch.device(device) if isinstance(device, str) else torch.device('cuda', device)
     cdev = dev if comm_device is None else comm_device
     timing = {}
     t0 = datetime.datetime.now()
@@ -242,7 +245,8 @@ def interpolate_day(sat, sie, x, y, mean, date='', T=9, radius=300, grid_res=25,
         xyt_d = torch.from_numpy(np.ascontiguousarray(
             np.stack([x_train[cat], y_train[cat], t_train[cat]], axis=1).reshape(-1, 3))).to(dev)
         z_d = torch.from_numpy(np.ascontiguousarray(z[cat])).to(dev)
-    torch.cuda.synchronize(dev)
+    if dev.type == 'cuda':
+        torch.cuda.synchronize(dev)
     timing['neighbours_s'] = (datetime.datetime.now() - t0).total_seconds()
 
     # pass 1 (GPR:258-261)
