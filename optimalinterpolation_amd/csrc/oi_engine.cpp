@@ -122,14 +122,15 @@ const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_ch
                                     "k_finalize", "k_predict"};
 
 // Panel scheme, read per call from OI_PANEL:
-//   1 (default): one-column left-looking panels, every column streams its
-//                whole block row of L (and of W = L^-1);
-//   2          : even/odd column pairs share one stream (k_panel_even +
-//                k_chol_panel(kbeg = j-1)): half the L / W traffic, measured
-//                equal in time on the day workload (round 1).
+//   2 (default): even/odd block-column pairs share one stream (k_panel_even +
+//                k_chol_panel(kbeg = j-1)): half the L / W traffic of the
+//                one-column scheme and k_scale only every other column;
+//                +2.5 % on the day workload;
+//   1          : one-column left-looking panels, every column streams its
+//                whole block row of L (and of W = L^-1).
 bool legacy_panels() {
   const char* e = getenv("OI_PANEL");
-  return !(e && atoi(e) == 2);
+  return e && atoi(e) == 1;
 }
 struct KStat {
   int64_t launches = 0;
