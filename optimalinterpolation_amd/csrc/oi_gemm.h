@@ -120,29 +120,6 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
   }
 }
 
-// D2 = Dj * S for a 64 x 128 S held in LDS as [k][n] (row stride LDSB), with
-// Dj a column-major 64x64 tile read straight from global memory as the A
-// operand (it is shared by all of a cell's workgroups: L2-resident).
-__device__ __forceinline__ void times_tile(Quad& acc2, const double* __restrict__ Dj,
-                                           const double* Ss) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wr = (w >> 2) & 1, wc = w & 3;
-  const int fr = lane & 15, fk = lane >> 4;
-  quad_zero(acc2);
-#pragma unroll 4
-  for (int kk = 0; kk < GNB / 4; ++kk) {
-    const int k = kk * 4 + fk;
-    const double a0 = Dj[k * GNB + 32 * wr + fr];
-    const double a1 = Dj[k * GNB + 32 * wr + 16 + fr];
-    const double b0 = Ss[k * LDSB + 32 * wc + fr];
-    const double b1 = Ss[k * LDSB + 32 * wc + 16 + fr];
-    acc2.c[0][0] = MFMA64(a0, b0, acc2.c[0][0]);
-    acc2.c[0][1] = MFMA64(a0, b1, acc2.c[0][1]);
-    acc2.c[1][0] = MFMA64(a1, b0, acc2.c[1][0]);
-    acc2.c[1][1] = MFMA64(a1, b1, acc2.c[1][1]);
-  }
-}
-
 // ---- 256-thread variant: one 64x64 output tile, wave w owns the 32x32
 // quadrant (32*(w>>1), 32*(w&1)); LDS 2 x (A, B) chunks of 16 x 80 = 40 KiB,
 // so four workgroups fit a CU.

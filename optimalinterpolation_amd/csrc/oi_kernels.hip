@@ -6,15 +6,18 @@
 //   k_build        K + sn2 I (Matern-3/2, GPR:93-94)                         O(n^2)
 //   k_diag_factor(j) factor + invert diagonal tile j: one wave per cell, rows in
 //                  registers (potrf + trti2, fully unrolled)             ~n^2 * 64
-//   k_chol_panel(j)  left-looking Cholesky, block column j, two row tiles per
-//                  512-thread workgroup sharing the L_j. panel:
-//                  L_ij^T = Dinv_jj (A_ij - sum_{k<j} L_ik L_jk^T)^T  (update and
-//                  triangular solve fused), the workgroup of the first tile
-//                  pair then applies the GEMM update of diagonal tile j+1
-//                  (look-ahead); plus row j of W = L^-1:
-//                  W_j,jj = -Dinv_jj sum_{k=jj}^{j-1} L_jk W_k,jj         2 n^3/3
+//   k_scale(j)     P_jk = -Dinv_jj L_jk (k < j; only k = j-1 at odd j)        ~n^2 * 64
+//   k_panel_even(j), j even: left-looking Cholesky for the column pair (j, j+1)
+//                  on one stream of block row i (64x128 blocks, 512 threads):
+//                  L_ij = sum_{k<j} L_ik P_jk^T + A_ij Dinv_jj^T  (update and
+//                  triangular solve in one GEMM loop), A_i,j+1 -= sum_{k<j}
+//                  L_ik L_j+1,k^T, look-ahead of diagonal tile j+1; rows j and
+//                  j+1 of W = L^-1 from one stream of W_k,jj
+//   k_chol_panel(j, kbeg = j-1), j odd: finishes column j / W row j with two
+//                  products per tile, look-ahead of tile j+1       (both) 2 n^3/3
+//                  (kbeg = 0: the one-column scheme, OI_PANEL=1)
 //   k_zvec/k_avec  z = W r, alpha = W^T z  (alpha = K^-1 r, GPR:127)          O(n^2)
-//   k_lauum_grad   K^-1 = W^T W, two tiles per workgroup, fused with the
+//   k_lauum_grad1  K^-1 = W^T W, one tile per workgroup, fused with the
 //                  gradient traces sum((K^-1 - alpha alpha^T) o dK_j); K and
 //                  dK_j are regenerated from coordinates (GPR:130-138)         n^3/3
 //   k_finalize     nlZ and dnlZ (GPR:128, GPR:131-138), fixed-order sums
@@ -88,22 +91,6 @@ __device__ __forceinline__ bool decode_tri(int x, int T, int& i, int& j) {
   while (ii * (ii + 1) / 2 > x) --ii;
   i = ii;
   j = x - ii * (ii + 1) / 2;
-  return true;
-}
-
-// lauum work slots: block row i owns floor(i/2)+1 column pairs (2J, 2J+1);
-// slots before row i: S(2a) = a(a+1), S(2a+1) = (a+1)^2
-__device__ __host__ __forceinline__ int lauum_slots_before(int i) {
-  const int a = i >> 1;
-  return (i & 1) ? (a + 1) * (a + 1) : a * (a + 1);
-}
-__device__ __forceinline__ bool decode_pair(int x, int T, int& i, int& J) {
-  if (x >= lauum_slots_before(T)) return false;
-  int ii = (int)(2.0 * sqrt((double)x));
-  while (ii > 0 && lauum_slots_before(ii) > x) --ii;
-  while (lauum_slots_before(ii + 1) <= x) ++ii;
-  i = ii;
-  J = x - lauum_slots_before(ii);
   return true;
 }
 
@@ -570,81 +557,11 @@ __global__ __launch_bounds__(256) void k_avec(const OiCell* __restrict__ cells,
 }
 
 // ------------------------------------------------------ k_lauum_grad
-// Tiles (i, j0), (i, j1=j0+1) of K^-1 = W^T W  (K^-1_ij = sum_{k>=i} W_ki^T W_kj)
-// fused with sum over the tiles of (K^-1 - alpha alpha^T) o {dK_0, dK_1, dK_2,
-// 2K} and the trace (GPR:130-138).  Strictly-lower entries count twice.
-__global__ __launch_bounds__(GEMM_THREADS) void k_lauum_grad(const OiCell* __restrict__ cells,
-                                                            const int32_t* __restrict__ list,
-                                                            int gx, int ncell) {
-  __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
-  int ci, slot;
-  if (!xcd_cell_slot(gx, ncell, ci, slot)) return;
-  const OiCell& c = cells[list[ci]];
-  const int T = c.T;
-  int i, J;
-  if (!decode_pair(slot, T, i, J)) return;
-  if (*c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
-  const int j0 = 2 * J, j1 = j0 + 1;
-  const bool has1 = j1 <= i;
-  Quad acc;
-  quad_zero(acc);
-  gemm2_kmajor(acc, lds, T - i, [&](int p, const double*& a, const double*& b0, const double*& b1) {
-    const int k = i + p;
-    a = tileW(c, k, i);
-    b0 = tileW(c, k, j0);
-    b1 = has1 ? tileW(c, k, j1) : g_zero_tile;
-  });
-  // coordinates of the rows (tile i) and the 128 columns (tiles j0, j1)
-  double* uQ = lds;              // [3][192]: rows 0..63, columns 64..191
-  double* uq = lds + 3 * 192;    // [3][192]
-  double* al = lds + 6 * 192;    // [192]
-  double* red = lds + 7 * 192;   // 8 waves x 5
-  const int t = threadIdx.x, n = c.n;
-  if (t < 192) {
-    const int a = t < 64 ? i * NB + t : j0 * NB + (t - 64);
-    for (int d = 0; d < 3; ++d) {
-      const double xv = a < n ? c.xyt[3 * a + d] : 0.0;
-      uQ[d * 192 + t] = (SQRT3 * xv) / c.hyp[d];
-      uq[d * 192 + t] = SQRT3 * (xv / c.hyp[d]);
-    }
-    al[t] = a < T * NB ? c.vec[T * NB + a] : 0.0;
-  }
-  __syncthreads();
-  const double sf2 = c.hyp[3];
-  double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int mb = 0; mb < 2; ++mb)
-    for (int nb = 0; nb < 2; ++nb)
-      for (int r = 0; r < 4; ++r) {
-        const int m = acc_row(mb, r), nc = acc_col(nb);
-        const int jh = nc < 64 ? j0 : j1, nn = nc & 63;
-        const int a = i * NB + m, b = jh * NB + nn;
-        if ((nc >= 64 && !has1) || a >= n || b >= n || (i == jh && m < nn)) continue;
-        const double wgt = (a == b) ? 1.0 : 2.0;
-        const double w = acc.c[mb][nb][r] - al[m] * al[64 + nc];
-        const double d0 = uQ[0 * 192 + m] - uQ[0 * 192 + 64 + nc];
-        const double d1 = uQ[1 * 192 + m] - uQ[1 * 192 + 64 + nc];
-        const double d2 = uQ[2 * 192 + m] - uQ[2 * 192 + 64 + nc];
-        const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-        const double e = exp(-Q);
-        const double K = sf2 * ((1.0 + Q) * e);
-        const double q0 = uq[0 * 192 + m] - uq[0 * 192 + 64 + nc];
-        const double q1 = uq[1 * 192 + m] - uq[1 * 192 + 64 + nc];
-        const double q2 = uq[2 * 192 + m] - uq[2 * 192 + 64 + nc];
-        s[0] += wgt * (w * (sf2 * ((q0 * q0) * e)));
-        s[1] += wgt * (w * (sf2 * ((q1 * q1) * e)));
-        s[2] += wgt * (w * (sf2 * ((q2 * q2) * e)));
-        s[3] += wgt * (w * (2.0 * K));
-        if (a == b) s[4] += w;
-      }
-  block_sum<5, 8>(s, red);
-  if (t == 0) {
-    double* pp = c.part + OI_PART_GRAD(0) + 5 * (size_t)slot;
-    for (int q = 0; q < 5; ++q) pp[q] = s[q];
-  }
-}
-
-// One-tile variant (256 threads, 40 KiB LDS -> 4 workgroups per CU): tile
-// (i, j) of K^-1 = sum_{k>=i} W_ki^T W_kj fused with the same gradient sums.
+// Tile (i, j) of K^-1 = W^T W (K^-1_ij = sum_{k>=i} W_ki^T W_kj), one 256-thread
+// workgroup per lower tile (40 KiB LDS -> 4 workgroups per CU), fused with
+// sum over the tile of (K^-1 - alpha alpha^T) o {dK_0, dK_1, dK_2, 2K} and the
+// trace (GPR:130-138); K and dK are regenerated from the coordinates.
+// Strictly-lower entries count twice.
 __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ cells,
                                                     const int32_t* __restrict__ list, int gx,
                                                     int ncell) {
@@ -712,13 +629,12 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
 // ---------------------------------------------------------- k_finalize
 // nlZ = r.alpha/2 + sum log diag L + n log(2 pi)/2 (GPR:128); dnlZ (GPR:131-138)
 __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cells,
-                                                  const int32_t* __restrict__ list,
-                                                  int one_tile_slots) {
+                                                  const int32_t* __restrict__ list) {
   const OiCell& c = cells[list[blockIdx.x]];
   if (c.mode != OI_MODE_EVAL) return;
   __shared__ double red[4 * 7];
   const int t = threadIdx.x, T = c.T, ntile = T * (T + 1) / 2;
-  const int nslot = one_tile_slots ? ntile : lauum_slots_before(T);
+  const int nslot = ntile;
   if (*c.status != OI_OK) {
     if (t < 7) c.out[t] = INFINITY;
     return;
@@ -867,15 +783,6 @@ __global__ void k_residual(const double* __restrict__ y, const double* __restric
 // ------------------------------------------------------------ launchers
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 static inline int ret() { return hipGetLastError() == hipSuccess ? 0 : -1; }
-// lauum variant: one-tile 256-thread kernel (default, OI_LAUUM=1) or the
-// two-tile 512-thread kernel (OI_LAUUM=0); measured equal within 3 % on the day
-static inline bool lauum_one_tile() {
-  static const int v = [] {
-    const char* e = getenv("OI_LAUUM");
-    return e ? atoi(e) : 1;
-  }();
-  return v == 1;
-}
 static inline unsigned grid1(int gx, int ncell) { return (unsigned)gx * (unsigned)((ncell + 7) & ~7); }
 
 extern "C" int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT,
@@ -940,15 +847,9 @@ extern "C" int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncel
 extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                                     void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  if (lauum_one_tile()) {
-    const int gx = maxT * (maxT + 1) / 2;
-    hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list,
-                       gx, ncell);
-  } else {
-    const int gx = lauum_slots_before(maxT);
-    hipLaunchKernelGGL(k_lauum_grad, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream),
-                       cells, list, gx, ncell);
-  }
+  const int gx = maxT * (maxT + 1) / 2;
+  hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,
+                     ncell);
   return ret();
 }
 
@@ -962,8 +863,7 @@ extern "C" int oi_launch_predict(const OiCell* cells, const int32_t* list, int n
 extern "C" int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell,
                                   void* stream) {
   if (ncell <= 0) return 0;
-  hipLaunchKernelGGL(k_finalize, dim3(ncell), dim3(256), 0, S(stream), cells, list,
-                     lauum_one_tile() ? 1 : 0);
+  hipLaunchKernelGGL(k_finalize, dim3(ncell), dim3(256), 0, S(stream), cells, list);
   return ret();
 }
 
