@@ -104,3 +104,19 @@ def test_day_two_ranks_equals_one():
     assert set(got[0]) == set(ref)
     for k in ref:
         assert np.array_equal(got[0][k], ref[k], equal_nan=True), k
+
+
+def test_day_no_ice_cells():
+    """A day whose ice mask is empty (GPR:248 IDs empty): every field NaN, no error."""
+    from optimalinterpolation_amd import day
+    saved = day._lib
+    try:
+        day._lib = FakeLib()
+        d = _day()
+        sie = np.full(d.sie.shape, np.nan)
+        res = day.interpolate_day(d.sat, sie, d.x, d.y, d.mean, date='d', device='cpu')
+    finally:
+        day._lib = saved
+    assert res.info['ncell'] == 0
+    for k, v in res.items():
+        assert v.shape == sie.shape and np.isnan(v).all(), k
