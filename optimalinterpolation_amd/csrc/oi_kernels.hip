@@ -155,20 +155,80 @@ __device__ __forceinline__ double rdlane(double v, int lane) {
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
+// One wave multiplies two 32x32 operands staged in LDS (row stride 33):
+// D[m][n] = sum_k A(m, k) B(k, n) with A(m, k) = a[m*33 + k] (row-major) and
+// B(k, n) = b[k*33 + n] (row-major) or b[n*33 + k] (b_rows_are_n), on 2x2
+// v_mfma_f64_16x16x4f64 blocks; the result goes to d[m*33 + n].
+__device__ __forceinline__ void wave_gemm32(const double* a, const double* b, bool b_rows_are_n,
+                                            double* d, double sign) {
+  const int l = threadIdx.x & 63, fr = l & 15, fk = l >> 4;
+  d4 acc[2][2];
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = 4 * kk + fk;
+    double av[2], bv[2];
+    for (int q = 0; q < 2; ++q) {
+      av[q] = a[(16 * q + fr) * 33 + k];
+      bv[q] = b_rows_are_n ? b[(16 * q + fr) * 33 + k] : b[k * 33 + 16 * q + fr];
+    }
+    for (int mb = 0; mb < 2; ++mb)
+      for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = MFMA64(av[mb], bv[nb], acc[mb][nb]);
+  }
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb)
+      for (int r = 0; r < 4; ++r) d[(16 * mb + fk + 4 * r) * 33 + 16 * nb + fr] = sign * acc[mb][nb][r];
+}
+
+// Factor + invert diagonal tile j: one 64-lane wave per cell, lane r holding
+// row r of the tile in registers; blocked 2 x 2 over 32-column halves so the
+// serial (v_readlane-broadcast) part is a quarter of the unblocked one:
+//   potrf of columns 0..31 over all 64 rows  -> L00, L10
+//   A11 -= L10 L10^T                          (MFMA, via LDS)
+//   potrf of A11                              -> L11
+//   trti2 of L11 and of L00 (LAPACK dtrti2 order within each)
+//   Inv10 = -Inv11 (L10 Inv00)                (two MFMA products)
 __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ cells,
                                                    const int32_t* __restrict__ list, int j) {
-  __shared__ double Tt[NB * 65];  // transpose buffer for the row-major W_jj
+  __shared__ double Tt[128 * 33];  // transpose buffer for the row-major W_jj (64 x 65); also the
+                                  // 32x33 staging areas of the blocked steps
   const OiCell& c = cells[list[blockIdx.x]];
   if (j >= c.T || *c.status != OI_OK) return;
   const int r = threadIdx.x;
+  const bool lo = r < 32;
   double* Y = tileL(c, j, j);
   double R[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) R[q] = Y[q * NB + r];  // row r of the column-major tile
-  // ---- potrf (right-looking): scale column cc by 1/sqrt(pivot), update the rest
+  double* S0 = Tt;             // 32 x 33
+  double* S1 = Tt + 32 * 33;   // 32 x 33
+  double* S2 = Tt + 64 * 33;   // 32 x 33
   bool ok = true;
+  // ---- potrf, columns 0..31 (all 64 rows: rows 32..63 become L10)
 #pragma unroll
-  for (int cc = 0; cc < NB; ++cc) {
+  for (int cc = 0; cc < 32; ++cc) {
+    const double d = rdlane(R[cc], cc);
+    ok = ok && !(d <= 0.0);
+    const double l = sqrt(d);
+    const double lr = r > cc ? R[cc] / l : 0.0;
+    R[cc] = r > cc ? lr : (r == cc ? l : R[cc]);
+#pragma unroll
+    for (int s2 = cc + 1; s2 < 32; ++s2) R[s2] -= lr * rdlane(R[cc], s2);
+  }
+  // ---- A11 -= L10 L10^T
+  if (!lo)
+#pragma unroll
+    for (int k = 0; k < 32; ++k) S0[(r - 32) * 33 + k] = R[k];
+  __syncthreads();
+  wave_gemm32(S0, S0, true, S1, 1.0);
+  __syncthreads();
+  if (!lo)
+#pragma unroll
+    for (int n = 0; n < 32; ++n) R[32 + n] -= S1[(r - 32) * 33 + n];
+  // ---- potrf of A11 (rows 32..63; rows 0..31 see lr = 0)
+#pragma unroll
+  for (int cc = 32; cc < NB; ++cc) {
     const double d = rdlane(R[cc], cc);
     ok = ok && !(d <= 0.0);
     const double l = sqrt(d);
@@ -198,16 +258,41 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
     const int ntile = c.T * (c.T + 1) / 2;
     c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
   }
-  // ---- trti2, last column first: x = Inv[r][cc+1..r] . L[cc+1..r][cc],
-  //      column cc := -x / L[cc][cc]   (LAPACK dtrti2 order)
+  // L10 stays staged in S0 (rows 32..63 of the factor, columns 0..31)
+  // ---- trti2 of L11 (columns 63..32), then of L00 (columns 31..0, k <= 31)
 #pragma unroll
-  for (int cc = NB - 1; cc >= 0; --cc) {
+  for (int cc = NB - 1; cc >= 32; --cc) {
     const double ajj = 1.0 / rdlane(R[cc], cc);
     double x = 0.0;
 #pragma unroll
     for (int k = cc + 1; k < NB; ++k) x += R[k] * rdlane(R[cc], k);
     R[cc] = r > cc ? -ajj * x : (r == cc ? ajj : R[cc]);
   }
+#pragma unroll
+  for (int cc = 31; cc >= 0; --cc) {
+    const double ajj = 1.0 / rdlane(R[cc], cc);
+    double x = 0.0;
+#pragma unroll
+    for (int k = cc + 1; k < 32; ++k) x += R[k] * rdlane(R[cc], k);
+    R[cc] = (lo && r > cc) ? -ajj * x : (r == cc ? ajj : R[cc]);
+  }
+  // ---- Inv10 = -Inv11 (L10 Inv00)
+  if (lo) {
+#pragma unroll
+    for (int n = 0; n < 32; ++n) S1[r * 33 + n] = R[n];  // Inv00 rows
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) S2[(r - 32) * 33 + k] = R[32 + k];  // Inv11 rows
+  }
+  __syncthreads();
+  wave_gemm32(S0, S1, false, Tt + 96 * 33, 1.0);  // Y = L10 Inv00 -> scratch after S2
+  __syncthreads();
+  wave_gemm32(S2, Tt + 96 * 33, false, S0, -1.0);  // Inv10 = -Inv11 Y -> S0
+  __syncthreads();
+  if (!lo)
+#pragma unroll
+    for (int n = 0; n < 32; ++n) R[n] = S0[(r - 32) * 33 + n];
+  __syncthreads();  // Tt is reused below
   double* Dj = tileD(c, j);
 #pragma unroll
   for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
