@@ -139,11 +139,17 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # collectives: RCCL ('nccl') by default; OI_DIST_BACKEND=gloo (collective
+    # payloads staged on the host) lets several ranks share one GPU, which is
+    # how the N>1 path is rehearsed on a 1-GPU box
+    backend = os.environ.get('OI_DIST_BACKEND', 'nccl')
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group('nccl')
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+        dist.init_process_group(backend)
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device('cuda', gpu)
+    cdev = torch.device('cpu') if backend == 'gloo' else dev  # where collective tensors live
     from optimalinterpolation_amd import _lib
 
     steps, opt, cfg = build_steps(args, rank, world)
@@ -162,7 +168,7 @@ def main():
     def run_step(k, profile):
         cells, xyt, z, h = dev_steps[k]
         return _lib.gpr_batch_device(xyt, z, cells.offs, cells.xs, cells.mean, x0=x0 if opt else None,
-                                     opt=opt, hyp=h, info=True, device=local, profile=profile)
+                                     opt=opt, hyp=h, info=True, device=gpu, profile=profile)
 
     for k in range(args.warmup):
         run_step(k, False)
@@ -175,12 +181,12 @@ def main():
     for k in range(args.warmup, args.warmup + args.steps):
         outs.append(run_step(k, True))
     # the single gather of posterior fields (ncell x 8 fp64) to rank 0 over RCCL
-    res = torch.from_numpy(np.concatenate([o[0] for o in outs])).to(dev)
+    res = torch.from_numpy(np.concatenate([o[0] for o in outs])).to(cdev)
     if world > 1:
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([res.shape[0]], device=dev))
+        sizes = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([res.shape[0]], device=cdev))
         mx = int(max(s.item() for s in sizes))
-        padded = torch.zeros((mx, 8), dtype=torch.float64, device=dev)
+        padded = torch.zeros((mx, 8), dtype=torch.float64, device=cdev)
         padded[:res.shape[0]] = res
         bufs = [torch.zeros_like(padded) for _ in range(world)] if rank == 0 else None
         dist.gather(padded, bufs, dst=0)
@@ -188,11 +194,11 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ncells_rank = sum(steps[k].ncell for k in range(args.warmup, args.warmup + args.steps))
-    tot = torch.tensor([float(ncells_rank)], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(ncells_rank)], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot)
     total_cells = float(tot.item())
