@@ -45,6 +45,8 @@ def parse():
     p.add_argument('--workload', default='day', choices=['day', 'dayshard', 'predict', 'single'])
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--no-prime', action='store_true',
+                   help='skip the untimed priming call (profiler runs: every dispatch is then a timed one)')
     p.add_argument('--cpu-cores', type=int, default=0, help='0: min(16, affinity)')
     p.add_argument('--out', default='')
     return p.parse_args()
@@ -185,8 +187,9 @@ def main():
 
     # library initialisation (context, arena, code objects): one untimed call on
     # 8 small cells -- not a step
-    prime = synthetic.make_cells([300] * 8, seed=12345)
-    _lib.gpr_batch(prime.xyt, prime.z, prime.offs, prime.xs, prime.mean, x0=x0, opt=True, device=gpu)
+    if not args.no_prime:
+        prime = synthetic.make_cells([300] * 8, seed=12345)
+        _lib.gpr_batch(prime.xyt, prime.z, prime.offs, prime.xs, prime.mean, x0=x0, opt=True, device=gpu)
     for k in range(args.warmup):
         run_step(k, False)
     _lib.profile_reset()

@@ -10,5 +10,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -n 1 gpurun_out/smoke.log
 timeout -k 10 900 python bench.py --out gpurun_out/bench.json > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
 cat gpurun_out/bench.json
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --out gpurun_out/bench_prof.json > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-prime --out gpurun_out/bench_prof.json > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
 find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \;
