@@ -197,8 +197,103 @@ def interpolate_day(sat, sie, x, y, mean, date='', T=9, radius=300, grid_res=25,
     reference's keys ``date+'_interp'`` ... ``'_interp_error_smth'``.
     ``pass1_rows`` (ncell x 8) skips the fit (tests of smoothing + pass 2).
     """
+    return interpolate_days([(sat, sie, mean, date)], x, y, T=T, radius=radius, grid_res=grid_res,
+                            x0=x0, neighbours=neighbours, rank=rank, world=world, device=device,
+                            group=group, partition=partition,
+                            pass1_rows=None if pass1_rows is None else [pass1_rows],
+                            comm_device=comm_device, **opt_kw)[0]
+
+
+class _Day:
+    """Per-day state of interpolate_days on this rank."""
+
+
+def _prepare_day(sat, sie, mean, date, x, y, T, rad, neighbours, rank, world, dev, device,
+                 partition, fixed, opt_kw):
+    """Training set (GPR:223-246), ice cells (GPR:248-249), neighbour query
+    (GPR:159) and the rank's gathered inputs in HBM, observations already
+    minus the day's prior mean (GPR:163)."""
     import torch
-    T_mid = T // 2
+    d = _Day()
+    d.sie, d.mean, d.date = sie, float(mean), date
+    x_train, y_train, t_train, z = training_set(sat, x, y)
+    d.n_train = len(z)
+    d.IDs = np.where(~np.isnan(sie))
+    X = np.array([x[d.IDs], y[d.IDs]]).T
+    d.ncell = X.shape[0]
+    d.xs_all = np.column_stack([X, np.full(d.ncell, float(T // 2))])
+    if neighbours == 'device':
+        pts = torch.from_numpy(np.ascontiguousarray(np.column_stack([x_train, y_train]))).to(dev)
+        cols = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x_train, y_train, t_train, z)]
+        qall = torch.from_numpy(np.ascontiguousarray(X)).to(dev)
+        d.counts = _count_neighbours(pts, qall, rad, device, opt_kw)
+    else:
+        from scipy.spatial import cKDTree
+        tree = cKDTree(np.array([x_train, y_train]).T)
+        id_lists = [tree.query_ball_point(x=X[i, :], r=rad) for i in range(d.ncell)]
+        d.counts = np.array([len(l) for l in id_lists], dtype=np.int64)
+    if partition == 'lpt':
+        parts = driver.lpt_partition(driver.cell_costs(d.counts, opt=not fixed), world)
+    else:
+        parts = [np.asarray(p, dtype=np.int64) for p in split(np.arange(d.ncell), world)]
+    d.mine = parts[rank]
+    if neighbours == 'device':
+        q = qall[torch.from_numpy(d.mine).to(dev)] if len(d.mine) else qall[:0]
+        d.offs, idx = _lib.ball_query_device(pts, q.contiguous(), rad, device=device, **opt_kw)
+        d.xyt, zz = _lib.gather_rows_device(cols, idx, device=device, **opt_kw)
+    else:
+        sel = [np.asarray(id_lists[c], dtype=np.int64) for c in d.mine]
+        d.offs = np.zeros(len(d.mine) + 1, dtype=np.int64)
+        d.offs[1:] = np.cumsum([len(s_) for s_ in sel])
+        cat = np.concatenate(sel) if sel else np.zeros(0, np.int64)
+        d.xyt = torch.from_numpy(np.ascontiguousarray(
+            np.stack([x_train[cat], y_train[cat], t_train[cat]], axis=1).reshape(-1, 3))).to(dev)
+        zz = torch.from_numpy(np.ascontiguousarray(z[cat])).to(dev)
+    # outputs - mX with mX = mean (GPR:163): the batched call then runs with a
+    # zero prior mean and fs = mean + k*.alpha is completed on the host -- the
+    # same two roundings as the reference's, so several days (different means)
+    # can share one call
+    d.r = zz - d.mean
+    d.xs = d.xs_all[d.mine]
+    return d
+
+
+def _batched_call(days, opt, x0, hyps, device, opt_kw):
+    """One oi_gpr_batch over the rank's cells of every day; returns per-day
+    (rows [k x 8], info [k x 4]) with fs completed by the day's mean."""
+    import torch
+    live = [d for d in days if len(d.mine)]
+    out = {id(d): (np.zeros((0, 8)), np.zeros((0, 4))) for d in days}
+    if not live:
+        return out
+    xyt = torch.cat([d.xyt for d in live]).contiguous()
+    r = torch.cat([d.r for d in live]).contiguous()
+    offs = np.concatenate([[0]] + [np.diff(d.offs) for d in live]).cumsum().astype(np.int64)
+    xs = np.concatenate([d.xs for d in live])
+    hyp = np.concatenate([hyps[id(d)] for d in live]) if not opt else None
+    rows, st, info = _lib.gpr_batch_device(xyt, r, offs, xs, 0.0, x0=x0 if opt else None, opt=opt,
+                                           hyp=hyp, info=True, device=device, **opt_kw)
+    a = 0
+    for d in live:
+        k = len(d.mine)
+        rr = rows[a:a + k].copy()
+        rr[:, 0] = d.mean + rr[:, 0]  # GPR:180 fs = mean + Kxsx^T A
+        out[id(d)] = (rr, np.asarray(info[a:a + k], dtype=np.float64))
+        a += k
+    return out
+
+
+def interpolate_days(days, x, y, T=9, radius=300, grid_res=25, x0=None, neighbours='device', rank=0,
+                     world=1, device=0, group=None, partition='lpt', pass1_rows=None,
+                     comm_device=None, **opt_kw):
+    """GPR:216-336 for several days at once (``days`` = list of (sat, sie,
+    mean, date) as for ``interpolate_day``; the reference script handles one
+    ``day`` per run, GPR:211).  Pass 1 of every day is ONE batched call over
+    all days' cells on this rank (cells are independent, so per-cell results
+    are bitwise those of day-by-day calls), then each day's hyper fields are
+    smoothed, then pass 2 is again one call.  Returns a list of per-day dicts
+    (rank 0; Nones elsewhere when world > 1)."""
+    import torch
     if x0 is None:
         x0 = [np.log(grid_res * 1000), np.log(grid_res * 1000), np.log(1.), np.log(1.), np.log(1.),
               np.log(.1)]
@@ -208,106 +303,75 @@ def interpolate_day(sat, sie, x, y, mean, date='', T=9, radius=300, grid_res=25,
     # a GPU (tests substitute the liboi calls)
     dev = torch.device(device) if isinstance(device, str) else torch.device('cuda', device)
     cdev = dev if comm_device is None else comm_device
+    rad = radius * 1000
     timing = {}
     t0 = datetime.datetime.now()
-    x_train, y_train, t_train, z = training_set(sat, x, y)
-    IDs = np.where(~np.isnan(sie))
-    X = np.array([x[IDs], y[IDs]]).T
-    ncell = X.shape[0]
-    xs_all = np.column_stack([X, np.full(ncell, float(T_mid))])
-    rad = radius * 1000
-
-    # neighbour query (GPR:159) -> per-rank cells -> gathered inputs in HBM
-    if neighbours == 'device':
-        pts = torch.from_numpy(np.ascontiguousarray(np.column_stack([x_train, y_train]))).to(dev)
-        cols = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x_train, y_train, t_train, z)]
-        qall = torch.from_numpy(np.ascontiguousarray(X)).to(dev)
-        counts = _count_neighbours(pts, qall, rad, device, opt_kw)
-    else:
-        from scipy.spatial import cKDTree
-        tree = cKDTree(np.array([x_train, y_train]).T)
-        id_lists = [tree.query_ball_point(x=X[i, :], r=rad) for i in range(ncell)]
-        counts = np.array([len(l) for l in id_lists], dtype=np.int64)
-    if partition == 'lpt':
-        parts = driver.lpt_partition(driver.cell_costs(counts, opt=pass1_rows is None), world)
-    else:
-        parts = [np.asarray(p, dtype=np.int64) for p in split(np.arange(ncell), world)]
-    mine = parts[rank]
-    if neighbours == 'device':
-        q = qall[torch.from_numpy(mine).to(dev)] if len(mine) else qall[:0]
-        offs, idx = _lib.ball_query_device(pts, q.contiguous(), rad, device=device, **opt_kw)
-        xyt_d, z_d = _lib.gather_rows_device(cols, idx, device=device, **opt_kw)
-    else:
-        sel = [np.asarray(id_lists[c], dtype=np.int64) for c in mine]
-        offs = np.zeros(len(mine) + 1, dtype=np.int64)
-        offs[1:] = np.cumsum([len(s) for s in sel])
-        cat = np.concatenate(sel) if sel else np.zeros(0, np.int64)
-        xyt_d = torch.from_numpy(np.ascontiguousarray(
-            np.stack([x_train[cat], y_train[cat], t_train[cat]], axis=1).reshape(-1, 3))).to(dev)
-        z_d = torch.from_numpy(np.ascontiguousarray(z[cat])).to(dev)
+    D = [_prepare_day(sat, sie, mean, date, x, y, T, rad, neighbours, rank, world, dev, device,
+                      partition, pass1_rows is not None, opt_kw) for sat, sie, mean, date in days]
     if dev.type == 'cuda':
         torch.cuda.synchronize(dev)
     timing['neighbours_s'] = (datetime.datetime.now() - t0).total_seconds()
 
-    # pass 1 (GPR:258-261)
+    # pass 1 (GPR:258-261), all days in one call
     t1 = datetime.datetime.now()
-    xs_mine = xs_all[mine]
     if pass1_rows is not None:
-        rows1 = np.asarray(pass1_rows, dtype=np.float64).reshape(-1, 8)[mine]
-        info1 = np.zeros((len(mine), 4))
-    elif len(mine):
-        rows1, st1, info1 = _lib.gpr_batch_device(xyt_d, z_d, offs, xs_mine, mean, x0=x0, opt=True,
-                                                  info=True, device=device, **opt_kw)
+        p1 = {id(d): (np.asarray(pr, dtype=np.float64).reshape(-1, 8)[d.mine], np.zeros((len(d.mine), 4)))
+              for d, pr in zip(D, pass1_rows)}
     else:
-        rows1, info1 = np.zeros((0, 8)), np.zeros((0, 4))
+        p1 = _batched_call(D, True, x0, None, device, opt_kw)
     timing['pass1_s'] = (datetime.datetime.now() - t1).total_seconds()
-    payload = np.column_stack([rows1, np.asarray(info1, dtype=np.float64)]) if len(mine) else np.zeros((0, 12))
-    if world > 1:
-        full = _allgather_rows(payload, mine, ncell, cdev, group)
-    else:
-        full = np.full((ncell, 12), np.nan)
-        full[mine] = payload
-    res = DayResult()
-    grids = {}
-    for k, key in enumerate(PASS1_KEYS):
-        g = np.zeros(sie.shape) * np.nan
-        g[IDs] = full[:, k]
-        grids[key] = g
-        res[date + '_' + key] = g
 
-    # smoothing (GPR:298-307), every rank the same fields on its own GPU
+    # per day: pass-1 rows to every rank, grids, smoothing (GPR:262-311)
     t2 = datetime.datetime.now()
-    sm = smooth_many([grids[k] for k in HYPER_KEYS], smooth_vmax(radius, T), sie, smooth_std(grid_res),
-                     device=device)
-    for k, key in enumerate(HYPER_KEYS):
-        res[date + '_' + key + '_smth'] = sm[k]
+    results, hyps = [], {}
+    for d in D:
+        rows1, info1 = p1[id(d)]
+        payload = np.column_stack([rows1, info1]) if len(d.mine) else np.zeros((0, 12))
+        if world > 1:
+            d.full = _allgather_rows(payload, d.mine, d.ncell, cdev, group)
+        else:
+            d.full = np.full((d.ncell, 12), np.nan)
+            d.full[d.mine] = payload
+        res = DayResult()
+        grids = {}
+        for k, key in enumerate(PASS1_KEYS):
+            g = np.zeros(d.sie.shape) * np.nan
+            g[d.IDs] = d.full[:, k]
+            grids[key] = g
+            res[d.date + '_' + key] = g
+        sm = smooth_many([grids[k] for k in HYPER_KEYS], smooth_vmax(radius, T), d.sie,
+                         smooth_std(grid_res), device=device)
+        for k, key in enumerate(HYPER_KEYS):
+            res[d.date + '_' + key + '_smth'] = sm[k]
+        # pass-2 hypers looked up at the cell (GPR:170-172)
+        hyps[id(d)] = np.column_stack([sm[k][d.IDs] for k in range(5)])[d.mine]
+        results.append(res)
     timing['smooth_s'] = (datetime.datetime.now() - t2).total_seconds()
 
-    # pass 2 (GPR:312-319): hypers looked up at the cell (GPR:170-172)
+    # pass 2 (GPR:312-319), all days in one call
     t3 = datetime.datetime.now()
-    hyp = np.column_stack([sm[k][IDs] for k in range(5)])[mine]
-    if len(mine):
-        rows2, _, _ = _lib.gpr_batch_device(xyt_d, z_d, offs, xs_mine, mean, opt=False, hyp=hyp,
-                                            device=device, **opt_kw)
-        rows2 = rows2[:, :2]
-    else:
-        rows2 = np.zeros((0, 2))
+    p2 = _batched_call(D, False, x0, hyps, device, opt_kw)
     timing['pass2_s'] = (datetime.datetime.now() - t3).total_seconds()
-    if world > 1:
-        full2 = driver.gather_rows(rows2, mine, ncell, device=cdev, group=group)
-        if rank != 0:
-            return None
-    else:
-        full2 = np.full((ncell, 2), np.nan)
-        full2[mine] = rows2
-    for k, key in enumerate(('interp_smth', 'interp_error_smth')):
-        g = np.zeros(sie.shape) * np.nan
-        g[IDs] = full2[:, k]
-        res[date + '_' + key] = g
-    timing['total_s'] = (datetime.datetime.now() - t0).total_seconds()
-    res.info = {'ncell': ncell, 'n_train': len(z), 'counts': counts, 'evals': full[:, 11],
-                'timing': timing, 'neighbours': neighbours}
-    return res
+    out = []
+    for d, res in zip(D, results):
+        rows2 = p2[id(d)][0][:, :2]
+        if world > 1:
+            full2 = driver.gather_rows(rows2, d.mine, d.ncell, device=cdev, group=group)
+            if rank != 0:
+                out.append(None)
+                continue
+        else:
+            full2 = np.full((d.ncell, 2), np.nan)
+            full2[d.mine] = rows2
+        for k, key in enumerate(('interp_smth', 'interp_error_smth')):
+            g = np.zeros(d.sie.shape) * np.nan
+            g[d.IDs] = full2[:, k]
+            res[d.date + '_' + key] = g
+        timing['total_s'] = (datetime.datetime.now() - t0).total_seconds()
+        res.info = {'ncell': d.ncell, 'n_train': d.n_train, 'counts': d.counts,
+                    'evals': d.full[:, 11], 'timing': dict(timing), 'neighbours': neighbours}
+        out.append(res)
+    return out
 
 
 def _count_neighbours(pts, q, rad, device, opt_kw):

@@ -161,3 +161,22 @@ def test_day_12p5km_grid_pass2():
     ids = np.where(~np.isnan(d.sie))
     a, b = res['d_interp_smth'][ids], ref['d_interp_smth'][ids]
     assert np.all(np.abs(a - b) <= 1e-10 * np.maximum(1.0, np.abs(b)))
+
+
+def test_multi_day_batch_equals_day_by_day():
+    """interpolate_days fits every day's cells in ONE batched call (days with
+    different prior means): per-day results are bitwise those of separate
+    interpolate_day calls (cells are independent; the mean is folded exactly)."""
+    days = []
+    for k in range(3):
+        d = _day(seed=20 + k, nx=40, ice=110e3, obs=450e3, cover=(0.02, 0.05))
+        days.append((d, 0.27 + 0.01 * k, '2018120%d' % k))
+    batched = day.interpolate_days([(d.sat, d.sie, m, dt) for d, m, dt in days], days[0][0].x,
+                                   days[0][0].y)
+    for (d, m, dt), res in zip(days, batched):
+        one = day.interpolate_day(d.sat, d.sie, d.x, d.y, m, date=dt)
+        assert set(res) == set(one)
+        for key in one:
+            assert same(res[key], one[key]), key
+        ids = np.where(~np.isnan(d.sie))
+        assert np.isfinite(res[dt + '_interp_smth'][ids]).all()
