@@ -168,13 +168,15 @@ def _allgather_rows(rows, mine, ncell, device, group=None):
     ks = [torch.zeros_like(k) for _ in range(world)]
     dist.all_gather(ks, k, group=group)
     kmax = max(int(x.item()) for x in ks)
+    full = np.full((ncell, m), np.nan)
+    if kmax == 0:  # every rank empty (e.g. a day without ice): no payload to exchange
+        return full
     pay = torch.zeros((kmax, m + 1), dtype=torch.float64, device=device)
     if len(mine):
         pay[:len(mine), 0] = torch.from_numpy(np.asarray(mine, dtype=np.float64))
         pay[:len(mine), 1:] = torch.from_numpy(rows)
     bufs = [torch.zeros_like(pay) for _ in range(world)]
     dist.all_gather(bufs, pay, group=group)
-    full = np.full((ncell, m), np.nan)
     for r in range(world):
         b = bufs[r][:int(ks[r].item())].cpu().numpy()
         full[b[:, 0].astype(np.int64)] = b[:, 1:]

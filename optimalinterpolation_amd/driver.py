@@ -53,6 +53,8 @@ def gather_rows(local_rows, local_idx, ncell, device=None, group=None):
     ks = [torch.zeros_like(k) for _ in range(world)]
     dist.all_gather(ks, k, group=group)
     kmax = int(max(int(x.item()) for x in ks))
+    if kmax == 0:  # every rank empty: nothing to exchange
+        return np.full((ncell, m), np.nan) if rank == 0 else None
     pay = torch.zeros((kmax, m + 1), dtype=torch.float64, device=device)
     if len(local_idx):
         pay[:len(local_idx), 0] = torch.from_numpy(np.asarray(local_idx, dtype=np.float64))

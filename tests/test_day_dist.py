@@ -120,3 +120,35 @@ def test_day_no_ice_cells():
     assert res.info['ncell'] == 0
     for k, v in res.items():
         assert v.shape == sie.shape and np.isnan(v).all(), k
+
+
+def _empty_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from optimalinterpolation_amd import day
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    day._lib = FakeLib()
+    d = _day()
+    sie = np.full(d.sie.shape, np.nan)
+    res = day.interpolate_day(d.sat, sie, d.x, d.y, d.mean, date='d', rank=rank, world=world,
+                              device='cpu')
+    q.put((rank, None if res is None else bool(all(np.isnan(v).all() for v in res.values()))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_day_two_ranks_no_ice():
+    """Both collectives are skipped consistently when no rank has a cell."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got[0] is True and got[1] is None
