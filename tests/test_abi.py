@@ -45,3 +45,40 @@ def test_log2pi_constant():
     src = open(os.path.join(ROOT, 'optimalinterpolation_amd', 'csrc', 'oi_kernels.hip')).read()
     val = float(re.search(r'#define LOG2PI ([0-9.e+-]+)', src).group(1))
     assert val == np.log(2 * np.pi)
+
+
+def test_argument_errors_without_gpu():
+    """API misuse is rejected with OI_E_ARG (-1) before any device work, so
+    these run on a CPU-only host (GPR3D's numerical failures are NOT errors)."""
+    import numpy as np
+    lib = _lib.load()
+    D = ctypes.POINTER(ctypes.c_double)
+    I64 = ctypes.POINTER(ctypes.c_int64)
+    p = lambda a, t: a.ctypes.data_as(ctypes.POINTER(t))
+    xyt = np.zeros((3, 3))
+    z = np.zeros(3)
+    xs = np.zeros((1, 3))
+    out = np.zeros((1, 8))
+    bad_offs = np.array([1, 3], dtype=np.int64)          # offs[0] must be 0
+    rc = lib.oi_gpr_batch(p(xyt, ctypes.c_double), p(z, ctypes.c_double), p(bad_offs, ctypes.c_int64), 1,
+                          p(xs, ctypes.c_double), 0.0, None, 0, None, p(out, ctypes.c_double), None, None,
+                          None)
+    assert rc == -1 and b'offs' in lib.oi_last_error()
+    offs = np.array([0, 3], dtype=np.int64)
+    rc = lib.oi_gpr_batch(p(xyt, ctypes.c_double), p(z, ctypes.c_double), p(offs, ctypes.c_int64), 1,
+                          p(xs, ctypes.c_double), 0.0, None, 1, None, p(out, ctypes.c_double), None, None,
+                          None)                               # opt=1 without x0
+    assert rc == -1 and b'x0' in lib.oi_last_error()
+    o = np.zeros(2, dtype=np.int64)
+    rc = lib.oi_ball_query(None, -1, p(xs[:, :2].copy(), ctypes.c_double), 1, 1.0, p(o, ctypes.c_int64),
+                           None, 0, None)
+    assert rc == -1
+    f = np.zeros((1, 4, 4))
+    m = np.zeros((4, 4))
+    k = np.ones((4, 4))
+    rc = lib.oi_smooth_fields(p(f, ctypes.c_double), 1, 4, 4, p(np.ones(1), ctypes.c_double),
+                              p(m, ctypes.c_double), 0.0, p(k, ctypes.c_double), 4,
+                              p(f.copy(), ctypes.c_double), None)   # even kernel size
+    assert rc == -1 and b'odd' in lib.oi_last_error()
+    assert lib.oi_gpr_batch(None, None, p(np.zeros(1, np.int64), ctypes.c_int64), 0, None, 0.0, None, 1,
+                            None, None, None, None, None) == 0   # empty batch is a no-op
