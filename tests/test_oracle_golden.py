@@ -62,3 +62,21 @@ def test_edge_n0_semantics():
     out = O.gp_cell(np.zeros((0, 3)), np.zeros(0), [4e6, 4e6, 4.0], 0.28, opt=True)
     assert out[0] == 0.28 and out[1] == 1.0 and out[2] == 0.0 and np.signbit(out[2])
     assert np.allclose(out[3:], [25000, 25000, 1, 1, 1], rtol=0, atol=1e-9)
+
+
+def test_nystrom_oracle_bitwise():
+    """oracle/nystrom_oracle.py == the notebook's own Nystroem / SMLII(approx) /
+    GPR(approx) (fixtures: tests/golden/make_nystrom_golden.py)."""
+    from oracle import nystrom_oracle as N
+    d = load_golden('nystrom.npz')
+    for c in range(len(d['nlz'])):
+        a, b = d['offs'][c], d['offs'][c + 1]
+        x, y, h, M = d['x'][a:b], d['y'][a:b], d['h'][c], int(d['M'][c])
+        f, g = N.neg_log_ml(h, x, y, M)
+        assert float(np.asarray(f).item()) == d['nlz'][c], c
+        assert _same(g, d['grad'][c]), c
+        fs, sd, sp = N.predict(x, y, d['xs'], list(np.exp(h[:3])), np.exp(h[3]), np.exp(h[4]),
+                               float(d['mean']), M)
+        assert float(np.asarray(fs).item()) == d['fs'][c], c
+        assert _same(np.asarray(sd).reshape(-1)[:1], d['sd'][c:c + 1]), c
+        assert float(sp) == d['sprior'][c], c
