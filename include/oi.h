@@ -118,6 +118,27 @@ int oi_gather_rows(const double* x_train, const double* y_train, const double* t
                    const double* z, int64_t M, const int64_t* idx, int64_t N, double* xyt,
                    double* zout, const oi_options* opts);
 
+/* ---- Nystrom variant (GP_example.ipynb code cell 1: Nystroem, SMLII and GPR
+ * with approx=True) -- the rank-M approximation of the notebook -----------
+ * Per cell c (rows offs[c] .. offs[c+1]-1):
+ *   xyt [N x 3] inputs, y [N] outputs minus the prior mean (the notebook's
+ *       SMLII receives y - mX; GPR subtracts `mean` itself -- pass z - mean)
+ *   sel [soffs[ncell]] inducing rows of each cell, 0-based within the cell
+ *       (NB1 Nystroem: sorted(np.random.choice(range(n), M, replace=False))
+ *       after np.random.seed(20); the caller draws them)
+ *   hyp [ncell x 5] LINEAR (ell_x, ell_y, ell_t, sf2, sn2) as GPR() takes them
+ *       (SMLII's log-hypers exponentiated by the caller)
+ *   xs  [ncell x 3] prediction targets (needed with pred)
+ *   nlz [ncell], grad [ncell x 5]: SMLII(approx=True) (NULL both to skip)
+ *   pred [ncell x 3]: (fs = mean + k*.A, sd, prior sd)  (NULL to skip)
+ *   status [ncell]: 0 ok, 1 eigh / Cholesky failed (NB1 LinAlgError):
+ *       nlZ = grad = +inf, fs = sd = NaN
+ * 1 <= M <= n per cell.  With opts->device_inputs xyt and y are device pointers. */
+int oi_nystrom_batch(const double* xyt, const double* y, const int64_t* offs, int64_t ncell,
+                     const int64_t* sel, const int64_t* soffs, const double* hyp,
+                     const double* xs, double mean, double* nlz, double* grad, double* pred,
+                     int32_t* status, const oi_options* opts);
+
 /* ---- host optimiser (scipy 1.15 CG restated; see csrc/cg.hpp) ---- */
 typedef struct oi_cg oi_cg;
 /* x0: 6 log-hypers. gtol/maxiter as in oi_options (maxiter < 0 => 1200). */

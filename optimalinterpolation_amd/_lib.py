@@ -34,7 +34,7 @@ c_int32_p = ctypes.POINTER(ctypes.c_int32)
 EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_create',
            'oi_cg_step', 'oi_cg_feed', 'oi_cg_result', 'oi_cg_destroy', 'oi_last_error',
            'oi_version', 'oi_profile_json', 'oi_profile_reset', 'oi_smooth_fields',
-           'oi_ball_query', 'oi_gather_rows')
+           'oi_ball_query', 'oi_gather_rows', 'oi_nystrom_batch')
 
 
 class OiOptions(ctypes.Structure):
@@ -98,6 +98,11 @@ def load():
                                        c_int64_p, ctypes.c_int64, c_double_p, c_double_p,
                                        ctypes.POINTER(OiOptions)]
         lib.oi_gather_rows.restype = ctypes.c_int
+        lib.oi_nystrom_batch.argtypes = [c_double_p, c_double_p, c_int64_p, ctypes.c_int64,
+                                         c_int64_p, c_int64_p, c_double_p, c_double_p,
+                                         ctypes.c_double, c_double_p, c_double_p, c_double_p,
+                                         c_int32_p, ctypes.POINTER(OiOptions)]
+        lib.oi_nystrom_batch.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -207,6 +212,41 @@ def nlml_grad_batch(xyt, y, mX, offs, h, **opt_kw):
                                 ctypes.byref(o))
     _check(rc)
     return nlz, grad, status
+
+
+def nystrom_batch(xyt, y, offs, sel, soffs, hyp, xs=None, mean=0.0, objective=True,
+                  predict=True, **opt_kw):
+    """oi_nystrom_batch: returns (nlz [ncell] | None, grad [ncell x 5] | None,
+    pred [ncell x 3] | None, status [ncell]).  ``hyp`` are LINEAR hypers
+    (ell_x, ell_y, ell_t, sf2, sn2) per cell; ``sel``/``soffs`` the ragged
+    inducing rows (0-based within each cell)."""
+    lib = load()
+    xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    sel = np.ascontiguousarray(sel, dtype=np.int64)
+    soffs = np.ascontiguousarray(soffs, dtype=np.int64)
+    ncell = len(offs) - 1
+    hyp = np.ascontiguousarray(hyp, dtype=np.float64).reshape(ncell, 5)
+    if offs[-1] != len(y) or xyt.shape[0] != len(y) or len(soffs) != ncell + 1 \
+            or soffs[-1] != len(sel):
+        raise ValueError("inconsistent ragged batch")
+    if predict:
+        xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(ncell, 3)
+    nlz = np.empty(ncell) if objective else None
+    grad = np.empty((ncell, 5)) if objective else None
+    pred = np.empty((ncell, 3)) if predict else None
+    status = np.zeros(ncell, dtype=np.int32)
+    o = options(**opt_kw)
+    rc = lib.oi_nystrom_batch(_ptr(xyt, ctypes.c_double), _ptr(y, ctypes.c_double),
+                              _ptr(offs, ctypes.c_int64), ncell, _ptr(sel, ctypes.c_int64),
+                              _ptr(soffs, ctypes.c_int64), _ptr(hyp, ctypes.c_double),
+                              _ptr(xs if predict else None, ctypes.c_double), float(mean),
+                              _ptr(nlz, ctypes.c_double), _ptr(grad, ctypes.c_double),
+                              _ptr(pred, ctypes.c_double), _ptr(status, ctypes.c_int32),
+                              ctypes.byref(o))
+    _check(rc)
+    return nlz, grad, pred, status
 
 
 class CG:

@@ -5,6 +5,9 @@ import os
 import re
 import subprocess
 
+import numpy as np
+import pytest
+
 from conftest import ROOT
 from optimalinterpolation_amd import _lib
 
@@ -82,3 +85,15 @@ def test_argument_errors_without_gpu():
     assert rc == -1 and b'odd' in lib.oi_last_error()
     assert lib.oi_gpr_batch(None, None, p(np.zeros(1, np.int64), ctypes.c_int64), 0, None, 0.0, None, 1,
                             None, None, None, None, None) == 0   # empty batch is a no-op
+
+
+def test_nystrom_argument_errors():
+    """oi_nystrom_batch rejects bad ragged batches before any device work."""
+    x = np.zeros((4, 3))
+    y = np.zeros(4)
+    with pytest.raises(_lib.OiError, match='M <= n'):
+        _lib.nystrom_batch(x, y, [0, 4], np.arange(5), [0, 5], np.ones((1, 5)), predict=False)
+    with pytest.raises(_lib.OiError, match='inducing index'):
+        _lib.nystrom_batch(x, y, [0, 4], np.array([0, 4]), [0, 2], np.ones((1, 5)), predict=False)
+    with pytest.raises(_lib.OiError, match='hypers'):
+        _lib.nystrom_batch(x, y, [0, 4], np.array([0, 1]), [0, 2], np.zeros((1, 5)), predict=False)
