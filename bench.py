@@ -16,8 +16,14 @@ context, workspace arena, code objects) -- not a step.  The timed region is
 bracketed by barrier + device synchronise on every rank, and the max over
 ranks is reported.
 
+`--workload nystrom` times the notebook's Nystrom variant instead
+(GP_example.ipynb code cell 5): cells of n = 4600
+observations, M = 925 inducing rows, fit by CG on the Nystrom
+objective + predict (oi_nystrom_fit_batch); weak scaling.  Per rank 32 cells
+(--nys-cells) of n = 4600, M = 925.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-                       [--workload day|dayshard|predict|single]
+                       [--workload day|dayshard|predict|single|nystrom]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -33,6 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 matrix (= vector) dense peak, spec
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
 NSHARDS = 8
 METRIC = "grid-cells/sec (full GP fit+predict), 25 km pan-Arctic day, fp64"
 
@@ -42,8 +49,9 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=1)
     p.add_argument('--warmup', type=int, default=0)
-    p.add_argument('--workload', default='day', choices=['day', 'dayshard', 'predict', 'single'])
+    p.add_argument('--workload', default='day', choices=['day', 'dayshard', 'predict', 'single', 'nystrom'])
     p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--nys-cells', type=int, default=0, help='nystrom workload: cells per rank-step')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-prime', action='store_true',
                    help='skip the untimed priming call (profiler runs: every dispatch is then a timed one)')
@@ -146,6 +154,132 @@ def cpu_baseline(sizes, evals, cores):
             "probe": res}
 
 
+# ----------------------------------------------------------------- nystrom
+NYS_N, NYS_M, NYS_CELLS = 4600, 925, 32
+
+NYS_PROBE = r'''
+import os, sys, time, json
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from oracle import nystrom_oracle as N
+from optimalinterpolation_amd import synthetic
+n, M = int(sys.argv[2]), int(sys.argv[3])
+cells = synthetic.make_cells([n], seed=77)
+x, z, xs = cells.cell(0)
+y = z - cells.mean
+h = np.log([2.5e4, 2.5e4, 1.0, 1.0, 0.1])
+t = time.perf_counter(); N.neg_log_ml(h, x, y, M); te = time.perf_counter() - t
+t = time.perf_counter(); N.predict(x, y, xs, list(np.exp(h[:3])), np.exp(h[3]), np.exp(h[4]), cells.mean, M)
+tp = time.perf_counter() - t
+print(json.dumps({"n": n, "M": M, "eval_s": te, "pred_s": tp}))
+'''
+
+
+def nystrom_cpu_baseline(evals, cores):
+    """The oracle (NB1 restated, bit-exact vs the notebook's functions) timed
+    for one SMLII(approx=True) evaluation + one GPR(approx=True) at n=4600,
+    M=925 with single-threaded OpenBLAS, scaled by the GPU run's measured
+    objective evaluations per cell, ``cores`` such processes in parallel."""
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+    t0 = time.time()
+    out = subprocess.run([sys.executable, '-c', NYS_PROBE, ROOT, str(NYS_N), str(NYS_M)],
+                         capture_output=True, text=True, env=env, timeout=600, check=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    t_cell = float(np.mean(evals)) * r['eval_s'] + r['pred_s']
+    return {"value": cores / t_cell, "unit": "grid-cells/s", "cores": cores, "kind": "port",
+            "sample": (f"oracle/nystrom_oracle.py (bit-exact vs GP_example.ipynb's Nystroem/SMLII/GPR) "
+                       f"timed for 1 SMLII(approx) eval ({r['eval_s']:.2f} s) + 1 GPR(approx) "
+                       f"({r['pred_s']:.2f} s) at n={NYS_N}, M={NYS_M}, 1 OpenBLAS thread "
+                       f"({time.time() - t0:.0f} s wall); x {float(np.mean(evals)):.1f} measured "
+                       f"evals/cell, {cores} such processes in parallel: extrapolated"),
+            "probe": r}
+
+
+def main_nystrom(args, torch, dist, world, rank, gpu, cdev):
+    from optimalinterpolation_amd import _lib, nystrom, synthetic
+    dev = torch.device('cuda', gpu)
+    x0 = nystrom.default_x0()
+    ncell = args.nys_cells or NYS_CELLS
+    steps = []
+    for k in range(args.warmup + args.steps):
+        cells = synthetic.make_cells([NYS_N] * ncell, seed=args.seed + 1000 * rank + k)
+        sel, soffs = nystrom._ragged_sel(cells.offs, NYS_M)
+        y = cells.z - cells.mean  # NB1 passes outputs - mX
+        steps.append((cells, sel, soffs, torch.from_numpy(cells.xyt).to(dev).contiguous(),
+                      torch.from_numpy(y).to(dev).contiguous()))
+    torch.cuda.synchronize()
+
+    def run(k, profile):
+        cells, sel, soffs, xd, yd = steps[k]
+        return _lib.nystrom_fit_batch(xd, yd, cells.offs, sel, soffs, x0, cells.xs, cells.mean,
+                                      device=gpu, device_inputs=True, profile=profile)
+
+    if not args.no_prime:  # library / rocBLAS / rocSOLVER initialisation, not a step
+        pc = synthetic.make_cells([300], seed=4321)
+        ps, po = nystrom._ragged_sel(pc.offs, 60)
+        _lib.nystrom_fit_batch(pc.xyt, pc.z - pc.mean, pc.offs, ps, po, x0, pc.xs, pc.mean, device=gpu)
+    for k in range(args.warmup):
+        run(k, False)
+    _lib.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = [run(k, True) for k in range(args.warmup, args.warmup + args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ncells = ncell * args.steps * world
+    info = np.concatenate([o[2] for o in outs])
+    evals = info[:, 3].astype(float)
+    kern = {k: v for k, v in _lib.profile_json()['kernels'].items() if k.startswith('nys_')}
+    dom = max(kern, key=lambda k: kern[k]['total_ms'])
+    kd = kern[dom]
+    sec = kd['total_ms'] / 1e3
+    if kd['flops'] > 0 and (kd['bytes'] == 0 or kd['flops'] / kd['bytes'] > 10):
+        ach, peak, unit, bound = kd['flops'] / sec / 1e12, PEAK_FP64_TFLOPS, "TFLOP/s", "mfma"
+    else:
+        ach, peak, unit, bound = kd['bytes'] / sec / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+    roofline = {"bound": bound, "kernel": dom, "achieved": round(ach, 3), "peak": peak, "unit": unit,
+                "frac": round(ach / peak, 4), "traffic": None,
+                "launches": kd['launches'], "avg_launch_ms": kd['total_ms'] / max(kd['launches'], 1),
+                "flops_per_launch": kd['flops'] / max(kd['launches'], 1),
+                "bytes_per_launch": kd['bytes'] / max(kd['launches'], 1),
+                "stages_ms": {k: round(v['total_ms'], 3) for k, v in kern.items()},
+                "stage_model": "per-cell stage of oi_nystrom.hip timed with HIP events; algorithmic "
+                               "flops (Ki GEMM 2 n^2 M, eigh 4 M^3 ...) / bytes (objective pass 8 n^2)"}
+    line = {"metric": "grid-cells/sec (Nystrom fit+predict, NB1 cell 5), fp64",
+            "value": round(ncells / dt, 4), "unit": "grid-cells/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded cells of the SURVEY §8d generator)",
+            "config": {"workload": f"Nystrom (GP_example.ipynb cell 5): {ncell} cells x n={NYS_N}, "
+                                   f"M={NYS_M} per rank per step, CG fit + predict",
+                       "cells_per_step": ncell * world},
+            "evals_per_cell": round(float(np.mean(evals)), 2), "roofline": roofline}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        try:
+            line["cpu_baseline"] = nystrom_cpu_baseline(evals, cores)
+        except Exception as e:
+            line["cpu_baseline"] = {"value": None, "error": repr(e)}
+    else:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, 'w') as f:
+                f.write(s + '\n')
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------- main
 def main():
     args = parse()
@@ -165,6 +299,8 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device('cuda', gpu)
     cdev = torch.device('cpu') if backend == 'gloo' else dev  # where collective tensors live
+    if args.workload == 'nystrom':
+        return main_nystrom(args, torch, dist, world, rank, gpu, cdev)
     from optimalinterpolation_amd import _lib
 
     steps, opt, cfg, scaling = build_steps(args, rank, world)

@@ -121,8 +121,8 @@ int oi_gather_rows(const double* x_train, const double* y_train, const double* t
 /* ---- Nystrom variant (GP_example.ipynb code cell 1: Nystroem, SMLII and GPR
  * with approx=True) -- the rank-M approximation of the notebook -----------
  * Per cell c (rows offs[c] .. offs[c+1]-1):
- *   xyt [N x 3] inputs, y [N] outputs minus the prior mean (the notebook's
- *       SMLII receives y - mX; GPR subtracts `mean` itself -- pass z - mean)
+ *   xyt [N x 3] inputs, y [N] outputs minus the prior mean (NB1 passes
+ *       outputs - mX to both SMLII and GPR; GPR adds `mean` back to fs)
  *   sel [soffs[ncell]] inducing rows of each cell, 0-based within the cell
  *       (NB1 Nystroem: sorted(np.random.choice(range(n), M, replace=False))
  *       after np.random.seed(20); the caller draws them)
@@ -138,6 +138,19 @@ int oi_nystrom_batch(const double* xyt, const double* y, const int64_t* offs, in
                      const int64_t* sel, const int64_t* soffs, const double* hyp,
                      const double* xs, double mean, double* nlz, double* grad, double* pred,
                      int32_t* status, const oi_options* opts);
+
+/* NB1 code cell 5 for a ragged batch: minimize(SMLII, x0, args=(x, y, True, M),
+ * method='CG', jac=True) per cell (the restated scipy CG, maxiter <0 => 1000 =
+ * len(x0)*200; gtol from opts), then GPR(approx=True, returnprior=True) at the
+ * fitted hypers.
+ *   x0  [5] initial log-hypers (NB1: log 25e3, log 25e3, 0, 0, log .1)
+ *   out [ncell x 8] (fs, sd, prior sd, ell_x, ell_y, ell_t, sf2, sn2)
+ *   status [ncell] as above at the fitted hypers; info [ncell x 4] or NULL:
+ *   (nit, cg_status, nfev, n_objective_evals).  Other arguments as above. */
+int oi_nystrom_fit_batch(const double* xyt, const double* y, const int64_t* offs, int64_t ncell,
+                         const int64_t* sel, const int64_t* soffs, const double* x0,
+                         const double* xs, double mean, double* out, int32_t* status,
+                         int32_t* info, const oi_options* opts);
 
 /* ---- host optimiser (scipy 1.15 CG restated; see csrc/cg.hpp) ---- */
 typedef struct oi_cg oi_cg;

@@ -34,7 +34,8 @@ c_int32_p = ctypes.POINTER(ctypes.c_int32)
 EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_create',
            'oi_cg_step', 'oi_cg_feed', 'oi_cg_result', 'oi_cg_destroy', 'oi_last_error',
            'oi_version', 'oi_profile_json', 'oi_profile_reset', 'oi_smooth_fields',
-           'oi_ball_query', 'oi_gather_rows', 'oi_nystrom_batch')
+           'oi_ball_query', 'oi_gather_rows', 'oi_nystrom_batch',
+           'oi_nystrom_fit_batch')
 
 
 class OiOptions(ctypes.Structure):
@@ -103,6 +104,11 @@ def load():
                                          ctypes.c_double, c_double_p, c_double_p, c_double_p,
                                          c_int32_p, ctypes.POINTER(OiOptions)]
         lib.oi_nystrom_batch.restype = ctypes.c_int
+        lib.oi_nystrom_fit_batch.argtypes = [c_double_p, c_double_p, c_int64_p, ctypes.c_int64,
+                                             c_int64_p, c_int64_p, c_double_p, c_double_p,
+                                             ctypes.c_double, c_double_p, c_int32_p, c_int32_p,
+                                             ctypes.POINTER(OiOptions)]
+        lib.oi_nystrom_fit_batch.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -247,6 +253,42 @@ def nystrom_batch(xyt, y, offs, sel, soffs, hyp, xs=None, mean=0.0, objective=Tr
                               ctypes.byref(o))
     _check(rc)
     return nlz, grad, pred, status
+
+
+def nystrom_fit_batch(xyt, y, offs, sel, soffs, x0, xs, mean, **opt_kw):
+    """oi_nystrom_fit_batch: returns (out [ncell x 8] = (fs, sd, prior sd, 5 linear
+    hypers), status [ncell], info [ncell x 4]).  With device_inputs=True, xyt
+    and y are torch device tensors."""
+    lib = load()
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    sel = np.ascontiguousarray(sel, dtype=np.int64)
+    soffs = np.ascontiguousarray(soffs, dtype=np.int64)
+    ncell = len(offs) - 1
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(5)
+    xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(ncell, 3)
+    if opt_kw.get('device_inputs'):
+        if xyt.numel() != 3 * offs[-1] or y.numel() != offs[-1]:
+            raise ValueError("inconsistent ragged batch")
+        px, py = _dptr(xyt), _dptr(y)
+    else:
+        xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        if offs[-1] != len(y) or xyt.shape[0] != len(y):
+            raise ValueError("inconsistent ragged batch")
+        px, py = _ptr(xyt, ctypes.c_double), _ptr(y, ctypes.c_double)
+    if len(soffs) != ncell + 1 or soffs[-1] != len(sel):
+        raise ValueError("inconsistent inducing rows")
+    out = np.empty((ncell, 8))
+    status = np.zeros(ncell, dtype=np.int32)
+    info = np.zeros((ncell, 4), dtype=np.int32)
+    o = options(**opt_kw)
+    rc = lib.oi_nystrom_fit_batch(px, py, _ptr(offs, ctypes.c_int64), ncell,
+                                  _ptr(sel, ctypes.c_int64), _ptr(soffs, ctypes.c_int64),
+                                  _ptr(x0, ctypes.c_double), _ptr(xs, ctypes.c_double), float(mean),
+                                  _ptr(out, ctypes.c_double), _ptr(status, ctypes.c_int32),
+                                  _ptr(info, ctypes.c_int32), ctypes.byref(o))
+    _check(rc)
+    return out, status, info
 
 
 class CG:

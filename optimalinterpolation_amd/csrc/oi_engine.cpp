@@ -156,6 +156,12 @@ struct RoundRec {
   double ms;    // GPU time of the round's launches
 };
 std::vector<RoundRec> g_rounds;  // every profiled round since the last reset
+// stages timed by the other translation units (oi_nystrom.hip), by name
+struct ExtStat {
+  int64_t launches = 0;
+  double ms = 0.0, flops = 0.0, bytes = 0.0;
+};
+std::vector<std::pair<std::string, ExtStat>> g_ext;
 
 // ------------------------------------------------------------- context
 struct Context {
@@ -868,6 +874,19 @@ const char* oi_last_error(void) { return g_last_error.c_str(); }
 // internal: lets the other translation units (oi_day.cpp) report errors
 int oi_set_last_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
 int32_t oi_version(void) { return OI_VERSION; }
+// internal: per-stage HIP-event timings from the other translation units
+void oi_profile_add(const char* name, int64_t launches, double ms, double flops, double bytes) {
+  std::lock_guard<std::mutex> pl(g_prof_mu);
+  for (auto& e : g_ext)
+    if (e.first == name) {
+      e.second.launches += launches;
+      e.second.ms += ms;
+      e.second.flops += flops;
+      e.second.bytes += bytes;
+      return;
+    }
+  g_ext.push_back({name, ExtStat{launches, ms, flops, bytes}});
+}
 
 int64_t oi_profile_json(char* buf, int64_t len) {
   std::lock_guard<std::mutex> pl(g_prof_mu);
@@ -877,6 +896,14 @@ int64_t oi_profile_json(char* buf, int64_t len) {
     std::snprintf(tmp, sizeof(tmp), "%s\"%s\":{\"launches\":%lld,\"total_ms\":%.6f,\"flops\":%.6e}",
                   k ? "," : "", kKernelName[k], (long long)g_prof[k].launches, g_prof[k].ms,
                   g_prof[k].flops);
+    s += tmp;
+  }
+  for (const auto& e : g_ext) {
+    char tmp[320];
+    std::snprintf(tmp, sizeof(tmp),
+                  ",\"%s\":{\"launches\":%lld,\"total_ms\":%.6f,\"flops\":%.6e,\"bytes\":%.6e}",
+                  e.first.c_str(), (long long)e.second.launches, e.second.ms, e.second.flops,
+                  e.second.bytes);
     s += tmp;
   }
   char tmp[256];
@@ -911,6 +938,7 @@ void oi_profile_reset(void) {
   for (auto& k : g_prof) k = KStat();
   g_run = RunStat();
   g_rounds.clear();
+  g_ext.clear();
 }
 
 }  // extern "C"

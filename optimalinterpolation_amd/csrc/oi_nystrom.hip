@@ -9,25 +9,37 @@
 //   s, u = eigh(Kmm); s[s<=0] = 1e-12; st = n s / M               (rocSOLVER syevd)
 //   ut = sqrt(M/n) Knm u / s;  C = Vi ut = ut / sn2                (rocBLAS gemm + kernel)
 //   B = diag(1/st) + ut' C;  L = chol(B)                           (gemm + potrf)
-//   alpha = L'^-1 L^-1 C';  Ki = Vi - C alpha;  A = Ki r           (trsm x2, gemm, gemv)
-//   objective: det = slogdet(sn2 I + (sqrt(st) ut)'(sqrt(st) ut)) / 2
-//              nlZ = r.A/2 + det + n log(2 pi)/2
-//              dnlZ_d = sum((Ki - A A') * dK_d)/2, dnlZ_3 = sum(Q * 2K)/2,
-//              dnlZ_4 = sn2 tr(Q)   -- exact K, dK (NB1 SMLII quirks kept)
-//   predict:   fs = mean + k*.A;  sd = sqrt(sf2 - k*' Ki k*);  prior sd = sqrt(sf2)
 //
-// The dense factorisations go to rocSOLVER / rocBLAS (plain library LAPACK /
-// GEMM on M x M and n x M panels); the n x n objective pass -- the only part
-// that touches every (i, j) pair -- is the fused kernel k_nys_grad: it
+// NB1 then forms alpha = L'^-1 L^-1 C' and Ki = Vi - C alpha (n x n).  Here
+// the same quantities come from W' = C L^-T (n x M: batched trtri of L, then
+// one GEMM -- rocBLAS trsm at these shapes runs at a few TFLOP/s):
+//   C alpha = W'W,  A = Ki r = r/sn2 - W'(W r),  k*'Ki k* = |k*|^2/sn2 - |W k*|^2
+// and, because D B D = H / sn2 for D = diag(sqrt(st)) and NB1's
+// H = sn2 I + (sqrt(st) ut)'(sqrt(st) ut),
+//   slogdet(H) = M log sn2 + sum log st + 2 sum log diag(L)
+// -- no second Cholesky.  Only the objective needs the n x n Ki = Vi - W'W
+// (one n x n x M GEMM), its lower triangle swept once by the fused kernel k_nys_grad, which
 // regenerates K and dK_d from the 3-D inputs in registers and reduces
-// (Ki - A A') against them in one sweep over Ki, so the n x n x 3 dK array the
-// notebook materialises never exists.  Everything for one call stays on one
-// stream; per-cell status comes back in a single copy at the end.
+// (Ki - A A') against them, so the n x n x 3 dK array the notebook
+// materialises never exists:
+//   nlZ = r.A/2 + slogdet(H)/2 + n log(2 pi)/2
+//   dnlZ_d = sum((Ki - A A') * dK_d)/2, dnlZ_3 = sum(Q * 2K)/2, dnlZ_4 = sn2 tr(Q)
+//   (exact K, dK: NB1 SMLII quirks kept)
+//   predict: fs = mean + k*.A;  sd = sqrt(sf2 - k*'Ki k*);  prior sd = sqrt(sf2)
+//
+// The dense factorisations are plain library LAPACK / GEMM (rocSOLVER /
+// rocBLAS).  rocSOLVER's syevd at M ~ 1000 is a long chain of small kernels
+// (~20 ms, latency-bound), so the cells of a call are dealt over several
+// LANES -- each its own stream, rocBLAS handle and workspace -- that run
+// concurrently; per-cell status comes back in one copy at the end.
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <memory>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -37,6 +49,8 @@
 #pragma clang fp contract(off)
 
 extern "C" int oi_set_last_error(int code, const char* msg);  // oi_engine.cpp
+extern "C" void oi_profile_add(const char* name, int64_t launches, double ms, double flops,
+                               double bytes);  // oi_engine.cpp
 
 namespace {
 
@@ -88,19 +102,23 @@ __global__ void k_nys_eigpost(double* __restrict__ s, int64_t M, int64_t n,
   st[k] = ((double)n * v) / (double)M;
 }
 
-// ut = sqrt(M/n) * U1 / s  (column k divided by s[k]);  C = ut / sn2 (= Vi ut);
-// Lt = sqrt(st) * ut (the objective's slogdet factor)
+// ut = sqrt(M/n) * U1 / s  (column k divided by s[k]);  C = ut / sn2 (= Vi ut)
 __global__ void k_nys_ut(const double* __restrict__ U1, int64_t n, int64_t M,
-                         const double* __restrict__ s, const double* __restrict__ st, double c,
-                         double isn2, double* __restrict__ ut, double* __restrict__ C,
-                         double* __restrict__ Lt) {
+                         const double* __restrict__ s, double c, double isn2,
+                         double* __restrict__ ut, double* __restrict__ C) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n * M) return;
   const int64_t k = e / n;
   const double u = (c * U1[e]) / s[k];
   ut[e] = u;
   C[e] = isn2 * u;
-  if (Lt) Lt[e] = sqrt(st[k]) * u;
+}
+
+// A = r / sn2 (Vi r; the W'(W r) part is subtracted by a gemv)
+__global__ void k_nys_vi(const double* __restrict__ r, int64_t n, double isn2,
+                         double* __restrict__ A) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) A[i] = isn2 * r[i];
 }
 
 // A[i + ld i] = d + A[i + ld i]  (d = dv[i] if dv, else 1/dv-free scalar; inv => 1/dv[i])
@@ -110,22 +128,6 @@ __global__ void k_nys_diag(double* __restrict__ A, int64_t m, int64_t ld,
   if (i >= m) return;
   const double a = dv ? (inv ? 1.0 / dv[i] : dv[i]) : d;
   A[i + ld * i] = a + A[i + ld * i];
-}
-
-// T[k + M i] = C[i + n k]   (C' as the right-hand side of the two solves)
-__global__ void k_nys_transpose(const double* __restrict__ C, int64_t n, int64_t M,
-                                double* __restrict__ T) {
-  __shared__ double t[32][33];
-  const int64_t i0 = (int64_t)blockIdx.x * 32, k0 = (int64_t)blockIdx.y * 32;
-  for (int r = threadIdx.y; r < 32; r += blockDim.y) {
-    const int64_t i = i0 + threadIdx.x, k = k0 + r;
-    if (i < n && k < M) t[r][threadIdx.x] = C[i + n * k];
-  }
-  __syncthreads();
-  for (int r = threadIdx.y; r < 32; r += blockDim.y) {
-    const int64_t k = k0 + threadIdx.x, i = i0 + r;
-    if (i < n && k < M) T[k + M * i] = t[threadIdx.x][r];
-  }
 }
 
 template <int NV>
@@ -152,47 +154,71 @@ __global__ void __launch_bounds__(256) k_nys_dot(const double* __restrict__ a,
   if (threadIdx.x == 0) out[0] = v[0];
 }
 
-// out[0] = sum_i log L[i + ld i]   (half the log-determinant of L L')
-__global__ void __launch_bounds__(256) k_nys_logdiag(const double* __restrict__ L, int64_t m,
-                                                     int64_t ld, double* __restrict__ out) {
-  __shared__ double red[4];
-  double v[1] = {0.0};
-  for (int64_t i = threadIdx.x; i < m; i += 256) v[0] += log(L[i + ld * i]);
-  block_sum<1>(v, red);
-  if (threadIdx.x == 0) out[0] = v[0];
+// per matrix b of a strided batch of Cholesky factors:
+//   res[b * NRES_ + 1] = sum_k log L_b[k + M k] + (sum_k log st_b[k]) / 2
+// (slogdet(H)/2 minus M log(sn2)/2; one block per matrix)
+__global__ void __launch_bounds__(256) k_nys_logdet(const double* __restrict__ L, int64_t M,
+                                                    int64_t strideL, const double* __restrict__ st,
+                                                    int64_t strideS, double* __restrict__ res,
+                                                    int64_t strideR) {
+  __shared__ double red[8];
+  const int64_t b = blockIdx.x;
+  L += b * strideL;
+  st += b * strideS;
+  double v[2] = {0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < M; i += 256) {
+    v[0] += log(L[i + M * i]);
+    v[1] += log(st[i]);
+  }
+  block_sum<2>(v, red);
+  if (threadIdx.x == 0) res[b * strideR + 1] = v[0] + v[1] / 2.0;
 }
 
-// The objective's n x n pass (NB1 SMLII, approx branch): per 64 x 64 tile of
-// Q = Ki - A A', the five sums  sum Q dK_0, sum Q dK_1, sum Q dK_2,
-// sum Q (2 K), tr Q  with K = sf2 (1+D) e^-D, dK_d = sf2 q_d^2 e^-D regenerated
-// from the scaled inputs (no n x n x 3 array).  Ki is read once, coalesced
-// along its columns; one partial row of 5 per tile.
+// zero the strict upper triangle of a column-major M x M matrix (potrf / trtri
+// leave the caller's upper triangle in place)
+__global__ void k_nys_zero_upper(double* __restrict__ A, int64_t M) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+  if (i < j) A[i + M * j] = 0.0;
+}
+
+// The objective's n x n pass (NB1 SMLII, approx branch): the five sums
+// sum Q dK_0, sum Q dK_1, sum Q dK_2, sum Q (2 K), tr Q over Q = Ki - A A',
+// K = sf2 (1+D) e^-D, dK_d = sf2 q_d^2 e^-D regenerated from the scaled
+// inputs (no n x n x 3 array).  Q and dK are symmetric and Ki is stored as its
+// lower triangle only (syrk), so the sweep covers 64 x 64 tiles on or below
+// the diagonal, weighting i > j by 2; one partial row of 5 per tile (zeros
+// above the diagonal), Ki read once, coalesced along its columns.
 __global__ void __launch_bounds__(256) k_nys_grad(const double* __restrict__ Ki,
                                                   const double* __restrict__ A,
                                                   const double* __restrict__ sc,
                                                   const double* __restrict__ sq, int64_t n,
                                                   double sf2, double* __restrict__ part) {
   __shared__ double red[4 * 5];
-  const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int64_t j0 = (int64_t)blockIdx.y * 64 + (threadIdx.x >> 6) * 16;
   double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (i < n) {
-    const double ci[3] = {sc[i * 3], sc[i * 3 + 1], sc[i * 3 + 2]};
-    const double qi[3] = {sq[i * 3], sq[i * 3 + 1], sq[i * 3 + 2]};
-    const double Ai = A[i];
-    const int64_t jend = j0 + 16 < n ? j0 + 16 : n;
-    for (int64_t j = j0; j < jend; ++j) {
-      const double Q = Ki[i + n * j] - Ai * A[j];
-      const double D = dist3(ci, sc + j * 3);
-      const double e = exp(-D);
-      const double K = sf2 * ((1.0 + D) * e);
-      for (int d = 0; d < 3; ++d) {
-        const double t = qi[d] - sq[j * 3 + d];
-        const double q = sqrt(t * t);
-        v[d] += Q * (sf2 * ((q * q) * e));
+  if (blockIdx.x >= blockIdx.y) {
+    const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int64_t j0 = (int64_t)blockIdx.y * 64 + (threadIdx.x >> 6) * 16;
+    if (i < n) {
+      const double ci[3] = {sc[i * 3], sc[i * 3 + 1], sc[i * 3 + 2]};
+      const double qi[3] = {sq[i * 3], sq[i * 3 + 1], sq[i * 3 + 2]};
+      const double Ai = A[i];
+      int64_t jend = j0 + 16 < n ? j0 + 16 : n;
+      jend = jend < i + 1 ? jend : i + 1;  // j <= i
+      for (int64_t j = j0; j < jend; ++j) {
+        const double Q = Ki[i + n * j] - Ai * A[j];
+        const double D = dist3(ci, sc + j * 3);
+        const double e = exp(-D);
+        const double K = sf2 * ((1.0 + D) * e);
+        const double w = j == i ? 1.0 : 2.0;
+        for (int d = 0; d < 3; ++d) {
+          // SGPkernel's q_d = pdist of one coordinate = sqrt(t*t) = |t| exactly
+          // (binary64, round-to-nearest), so q_d^2 = fl(t*t): no sqrt needed
+          const double t = qi[d] - sq[j * 3 + d];
+          v[d] += w * (Q * (sf2 * ((t * t) * e)));
+        }
+        v[3] += w * (Q * (2.0 * K));
+        if (j == i) v[4] += Q;
       }
-      v[3] += Q * (2.0 * K);
-      if (j == i) v[4] += Q;
     }
   }
   block_sum<5>(v, red);
@@ -233,23 +259,6 @@ struct HipErr {
   } while (0)
 #define KC() HC(hipGetLastError())
 
-struct DBuf {
-  void* p = nullptr;
-  DBuf() = default;
-  explicit DBuf(size_t bytes) {
-    if (bytes) HC(hipMalloc(&p, bytes));
-  }
-  ~DBuf() {
-    if (p) (void)hipFree(p);
-  }
-  DBuf(const DBuf&) = delete;
-  DBuf& operator=(const DBuf&) = delete;
-  template <class T>
-  T* as() const {
-    return static_cast<T*>(p);
-  }
-};
-
 struct Handle {
   rocblas_handle h = nullptr;
   Handle() { BC(rocblas_create_handle(&h)); }
@@ -258,12 +267,588 @@ struct Handle {
   }
 };
 
+// opts.profile: HIP events around each stage of each cell, summed per stage
+// into oi_profile_json (algorithmic flops / bytes per stage alongside)
+enum { S_BUILD, S_EIGH, S_PANEL, S_KI, S_APPLY, S_LOGDET, S_GRAD, S_PRED, S_COUNT };
+const char* kStage[S_COUNT] = {"nys_build", "nys_eigh",   "nys_panels", "nys_ki_gemm",
+                               "nys_apply", "nys_logdet", "nys_grad",   "nys_predict"};
+struct Stager {
+  bool on = false;
+  hipStream_t st = nullptr;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> kind;
+  std::vector<double> fl, by;
+  void begin(int k, double flops, double bytes) {
+    if (!on) return;
+    kind.push_back(k);
+    fl.push_back(flops);
+    by.push_back(bytes);
+    rec();
+  }
+  void end() {
+    if (on) rec();
+  }
+  void rec() {
+    hipEvent_t e;
+    HC(hipEventCreate(&e));
+    ev.push_back(e);
+    HC(hipEventRecord(e, st));
+  }
+  void flush() {  // after the stream has been synchronised
+    if (!on) return;
+    double ms[S_COUNT] = {}, f[S_COUNT] = {}, b[S_COUNT] = {};
+    int64_t n[S_COUNT] = {};
+    for (size_t q = 0; q < kind.size(); ++q) {
+      float t = 0.f;
+      HC(hipEventElapsedTime(&t, ev[2 * q], ev[2 * q + 1]));
+      ms[kind[q]] += t;
+      f[kind[q]] += fl[q];
+      b[kind[q]] += by[q];
+      n[kind[q]] += 1;
+    }
+    for (int k = 0; k < S_COUNT; ++k)
+      if (n[k]) oi_profile_add(kStage[k], n[k], ms[k], f[k], b[k]);
+    for (auto e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    kind.clear();
+    fl.clear();
+    by.clear();
+  }
+  ~Stager() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+};
+
 inline unsigned blocks(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
-// per-cell device results: [r.A, sum log diag(chol(H)), g0..g4 raw sums, k*.A, k*'Ki k*]
-constexpr int NRES = 9;
-// per-cell rocSOLVER infos: [syevd, potrf(B), potrf(H)]
-constexpr int NINFO = 3;
+// per-cell device results: [r.A, sum log diag(L) + sum log st / 2, g0..g4 raw
+// sums, k*.A, |k*|^2, |W k*|^2]
+constexpr int NRES = 10;
+// per-cell rocSOLVER infos: [syevd, potrf(B)]
+constexpr int NINFO = 2;
+
+}  // namespace
+
+namespace {
+
+// Validated ragged batch + the device-side state of one liboi call.
+struct Batch {
+  const double* xyt;
+  const double* y;
+  const int64_t* offs;
+  int64_t ncell;
+  const int64_t* sel;
+  const int64_t* soffs;
+  int64_t nmax = 0, mmax = 0;
+};
+
+int check_batch(Batch& b) {
+  if (b.ncell < 0) return oi_set_last_error(OI_E_ARG, "negative ncell");
+  if (b.ncell == 0) return 0;
+  if (!b.offs || !b.soffs || !b.sel || !b.xyt || !b.y) return oi_set_last_error(OI_E_ARG, "null pointer");
+  if (b.offs[0] != 0 || b.soffs[0] != 0) return oi_set_last_error(OI_E_ARG, "offs[0] must be 0");
+  for (int64_t c = 0; c < b.ncell; ++c) {
+    const int64_t n = b.offs[c + 1] - b.offs[c], M = b.soffs[c + 1] - b.soffs[c];
+    if (n < 1 || M < 1 || M > n) return oi_set_last_error(OI_E_ARG, "each cell needs 1 <= M <= n");
+    for (int64_t k = b.soffs[c]; k < b.soffs[c + 1]; ++k)
+      if (b.sel[k] < 0 || b.sel[k] >= n)
+        return oi_set_last_error(OI_E_ARG, "inducing index out of range");
+    b.nmax = n > b.nmax ? n : b.nmax;
+    b.mmax = M > b.mmax ? M : b.mmax;
+  }
+  if (b.nmax > INT32_MAX / 2) return oi_set_last_error(OI_E_ARG, "cell too large");
+  return 0;
+}
+
+int setup(const oi_options* opts, oi_options& o) {
+  oi_options_default(&o);
+  if (opts) o = *opts;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return oi_set_last_error(OI_E_NODEV, "no HIP device available");
+  if (o.device < 0 || o.device >= ndev) return oi_set_last_error(OI_E_ARG, "bad device ordinal");
+  if (hipSetDevice(o.device) != hipSuccess) return oi_set_last_error(OI_E_HIP, "hipSetDevice failed");
+  return 0;
+}
+
+// Outcome of one cell at one hyper point (host side).
+struct CellOut {
+  double nlz, grad[5], fs, sd, sprior;
+  int status;
+};
+
+// One lane: a stream, a rocBLAS handle and the workspace for the largest cell.
+struct Buf {
+  void* p = nullptr;
+  Buf() = default;
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  void alloc(size_t bytes) {
+    if (bytes) HC(hipMalloc(&p, bytes));
+  }
+  ~Buf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+struct Lane {
+  hipStream_t st = nullptr;
+  Handle H;
+  Buf Knm, U1, ut, W, Ki, Av, tv, ks, kv, xsc, part;
+  Stager sg;
+  hipEvent_t done = nullptr;
+  Lane(int64_t nmax, int64_t mmax, bool obj, bool pred, bool profile) {
+    HC(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HC(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    BC(rocblas_set_stream(H.h, st));
+    const int64_t nM = nmax * mmax, nt = blocks(nmax, 64);
+    Knm.alloc(nM * 8);
+    U1.alloc(nM * 8);
+    ut.alloc(nM * 8);
+    W.alloc(nM * 8);
+    Av.alloc(nmax * 8);
+    tv.alloc(mmax * 8);
+    if (obj) {
+      Ki.alloc(nmax * nmax * 8);
+      part.alloc(nt * nt * 5 * 8);
+    }
+    if (pred) {
+      ks.alloc(nmax * 8);
+      kv.alloc(mmax * 8);
+      xsc.alloc(3 * 8);
+    }
+    sg.on = profile;
+    sg.st = st;
+  }
+  ~Lane() {
+    if (done) (void)hipEventDestroy(done);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+// Evaluates any subset of a validated batch's cells at given LINEAR hypers.
+//
+// rocSOLVER's syevd / potrf at M ~ 1000 are long chains of small kernels
+// (~20 ms / ~2.4 ms for one matrix, latency-bound); their strided-batched
+// forms factor 8 such matrices in ~1.4x the time of one.  So a run is
+// phase-major over CHUNKS of cells (sorted by M, so equal-M cells are
+// adjacent slots): (1) K_mm of every cell, (2) one batched syevd per equal-M
+// group, (3) the n x M panels and B of every cell, (4) one batched potrf per
+// group, (5) the triangular solve, objective and prediction of every cell.
+// Per-cell phases are dealt round-robin over LANES (OI_NYS_LANES, default 1:
+// stream + rocBLAS handle + scratch each; more lanes measured no faster with
+// the box's 4 hardware queues); per-slot state (scaled inputs,
+// K_mm -> u, s, st, C, B -> L) lives in chunk-sized slot arrays.
+class Runner {
+ public:
+  // own_stream: work on a private stream (several Runners then overlap);
+  // otherwise on the caller's opts.stream
+  Runner(const Batch& b, const oi_options& o, bool want_obj, bool want_pred, const double* xs,
+         bool own_stream = false)
+      : b_(b), st_((hipStream_t)o.stream), alloc_obj_(want_obj), alloc_pred_(want_pred) {
+    if (own_stream) {
+      HC(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+      own_ = true;
+    }
+    const int64_t N = b.offs[b.ncell], S = b.soffs[b.ncell];
+    dx_ = b.xyt;
+    dy_ = b.y;
+    if (!o.device_inputs) {
+      hx_.alloc(N * 3 * 8);
+      hy_.alloc(N * 8);
+      HC(hipMemcpyAsync(hx_.p, b.xyt, N * 3 * 8, hipMemcpyHostToDevice, st_));
+      HC(hipMemcpyAsync(hy_.p, b.y, N * 8, hipMemcpyHostToDevice, st_));
+      dx_ = hx_.as<double>();
+      dy_ = hy_.as<double>();
+    }
+    dsel_.alloc(S * 8);
+    HC(hipMemcpyAsync(dsel_.p, b.sel, S * 8, hipMemcpyHostToDevice, st_));
+    if (want_pred) {
+      dxs_.alloc(b.ncell * 3 * 8);
+      HC(hipMemcpyAsync(dxs_.p, xs, b.ncell * 3 * 8, hipMemcpyHostToDevice, st_));
+    }
+    res_.alloc(b.ncell * NRES * 8);
+    info_.alloc(b.ncell * NINFO * sizeof(rocblas_int));
+    HC(hipHostMalloc((void**)&hr_, b.ncell * NRES * 8, hipHostMallocDefault));
+    HC(hipHostMalloc((void**)&hi_, b.ncell * NINFO * sizeof(rocblas_int), hipHostMallocDefault));
+    BC(rocblas_set_stream(H_.h, st_));
+    sg_.on = o.profile != 0;
+    sg_.st = st_;
+    int nl = 1;
+    if (const char* e = getenv("OI_NYS_LANES")) nl = atoi(e);
+    nl = nl < 1 ? 1 : nl;
+    nl = nl > b.ncell ? (int)b.ncell : nl;
+    for (int l = 0; l < nl; ++l)
+      lanes_.emplace_back(new Lane(b.nmax, b.mmax, want_obj, want_pred, o.profile != 0));
+    // slot arrays: sc, sq (n x 3), Kmm (M^2), s, st, E (M), C (n x M), B (M^2);
+    // chunk <= 64 cells and <= 1/4 of the free HBM
+    const int64_t nmax = b.nmax, mmax = b.mmax;
+    const size_t per = (size_t)(6 * nmax + 2 * mmax * mmax + 3 * mmax + nmax * mmax) * 8;
+    size_t fr = 0, tot = 0;
+    HC(hipMemGetInfo(&fr, &tot));
+    int64_t ch = std::min<int64_t>(64, b.ncell);
+    ch = std::min<int64_t>(ch, std::max<int64_t>(1, (int64_t)(fr / 4 / per)));
+    chunk_ = ch;
+    sc_.alloc(ch * nmax * 3 * 8);
+    sq_.alloc(ch * nmax * 3 * 8);
+    Kmm_.alloc(ch * mmax * mmax * 8);
+    eval_.alloc(ch * mmax * 8);
+    stl_.alloc(ch * mmax * 8);
+    E_.alloc(ch * mmax * 8);
+    C_.alloc(ch * nmax * mmax * 8);
+    B_.alloc(ch * mmax * mmax * 8);
+    info_tmp_.alloc(2 * ch * sizeof(rocblas_int));
+    HC(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+  }
+  ~Runner() {
+    if (own_ && st_) (void)hipStreamSynchronize(st_);
+    for (Lane* l : lanes_) delete l;
+    if (ready_) (void)hipEventDestroy(ready_);
+    if (hr_) (void)hipHostFree(hr_);
+    if (hi_) (void)hipHostFree(hi_);
+    if (own_ && st_) (void)hipStreamDestroy(st_);
+  }
+
+  // cells[k] at LINEAR hypers hyp[k*5 ..]; results into out[k]
+  void run(const std::vector<int64_t>& cells, const double* hyp, double mean, CellOut* out,
+           bool want_obj, bool want_pred) {
+    enqueue(cells, hyp, mean, want_obj, want_pred);
+    collect(out);
+  }
+
+  // queue one evaluation of cells[k] at hyp[k*5 ..] (copied) without waiting
+  void enqueue(const std::vector<int64_t>& cells, const double* hyp, double mean, bool want_obj,
+               bool want_pred) {
+    const int64_t nc = (int64_t)cells.size();
+    ncq_ = nc;
+    if (!nc) return;
+    if ((want_obj && !alloc_obj_) || (want_pred && !alloc_pred_))
+      throw HipErr{"Runner: stage not allocated"};
+    obj_ = want_obj;
+    pred_ = want_pred;
+    mean_ = mean;
+    cellv_ = cells;
+    hypv_.assign(hyp, hyp + nc * 5);
+    cells_ = &cellv_;
+    hyp_ = hypv_.data();
+    // positions sorted by M (equal-M cells adjacent for the batched factorisations)
+    order_.resize(nc);
+    for (int64_t k = 0; k < nc; ++k) order_[k] = k;
+    std::stable_sort(order_.begin(), order_.end(), [&](int64_t a, int64_t c) {
+      return Mof(cells[a]) < Mof(cells[c]);
+    });
+    HC(hipMemsetAsync(res_.p, 0, nc * NRES * 8, st_));
+    HC(hipMemsetAsync(info_.p, 0, nc * NINFO * sizeof(rocblas_int), st_));
+    for (int64_t p0 = 0; p0 < nc; p0 += chunk_) {
+      const int64_t p1 = std::min(nc, p0 + chunk_);
+      lanes_phase(p0, p1, 1);
+      batched(p0, p1, 0);
+      lanes_phase(p0, p1, 3);
+      batched(p0, p1, 1);
+      lanes_phase(p0, p1, 5);
+    }
+    HC(hipMemcpyAsync(hr_, res_.p, nc * NRES * 8, hipMemcpyDeviceToHost, st_));
+    HC(hipMemcpyAsync(hi_, info_.p, nc * NINFO * sizeof(rocblas_int), hipMemcpyDeviceToHost, st_));
+  }
+
+  // wait for the queued evaluation; out[k] for the enqueued cells[k]
+  void collect(CellOut* out) {
+    const int64_t nc = ncq_;
+    if (!nc) return;
+    const std::vector<int64_t>& cells = cellv_;
+    const double* hyp = hyp_;
+    const double mean = mean_;
+    HC(hipStreamSynchronize(st_));
+    sg_.flush();
+    for (Lane* l : lanes_) l->sg.flush();
+    const double inf = INFINITY, nan = NAN;
+    for (int64_t p = 0; p < nc; ++p) {
+      const int64_t k = order_[p], c = cells[k];
+      const int64_t n = b_.offs[c + 1] - b_.offs[c], M = Mof(c);
+      const double sf2 = hyp[k * 5 + 3], sn2 = hyp[k * 5 + 4];
+      const double* rr = hr_ + p * NRES;
+      const rocblas_int* ii = hi_ + p * NINFO;
+      const bool bad = ii[0] != 0 || ii[1] != 0;  // NB1's LinAlgError (eigh / cholesky)
+      CellOut& r = out[k];
+      r.status = bad ? 1 : 0;
+      if (obj_) {
+        if (bad) {
+          r.nlz = inf;
+          for (int q = 0; q < 5; ++q) r.grad[q] = inf;
+        } else {
+          // det = slogdet(H)/2 = (M log sn2 + sum log st + 2 sum log diag L) / 2
+          const double det = (double)M * std::log(sn2) / 2.0 + rr[1];
+          r.nlz = (rr[0] / 2.0 + det) + (double)n * std::log(2.0 * M_PI) / 2.0;
+          r.grad[0] = rr[2] / 2.0;
+          r.grad[1] = rr[3] / 2.0;
+          r.grad[2] = rr[4] / 2.0;
+          r.grad[3] = rr[5] / 2.0;
+          r.grad[4] = sn2 * rr[6];
+        }
+      }
+      if (pred_) {
+        const double err = rr[8] / sn2 - rr[9];  // k*'Ki k* = |k*|^2/sn2 - |W k*|^2
+        r.fs = bad ? nan : mean + rr[7];
+        r.sd = bad ? nan : std::sqrt(sf2 - err);
+        r.sprior = std::sqrt(sf2);
+      }
+    }
+  }
+
+ private:
+  int64_t Mof(int64_t c) const { return b_.soffs[c + 1] - b_.soffs[c]; }
+
+  // per-cell phase `ph` for positions [p0, p1) dealt over the lanes, fenced
+  // against the main stream on both sides
+  void lanes_phase(int64_t p0, int64_t p1, int ph) {
+    const int64_t nl = std::min<int64_t>((int64_t)lanes_.size(), p1 - p0);
+    HC(hipEventRecord(ready_, st_));
+    for (int64_t l = 0; l < nl; ++l) HC(hipStreamWaitEvent(lanes_[l]->st, ready_, 0));
+    for (int64_t p = p0; p < p1; ++p) {
+      Lane& L = *lanes_[(p - p0) % nl];
+      if (ph == 1) phase1(L, p, p - p0);
+      else if (ph == 3) phase3(L, p, p - p0);
+      else phase5(L, p, p - p0);
+    }
+    for (int64_t l = 0; l < nl; ++l) {
+      HC(hipEventRecord(lanes_[l]->done, lanes_[l]->st));
+      HC(hipStreamWaitEvent(st_, lanes_[l]->done, 0));
+    }
+  }
+
+  // which = 0: s, u = eigh(Kmm) (syevd); 1: L = chol(B) (potrf) -- one
+  // strided-batched call per equal-M run of slots, on the main stream
+  void batched(int64_t p0, int64_t p1, int which) {
+    const int64_t mm = b_.mmax * b_.mmax;
+    for (int64_t g0 = p0; g0 < p1;) {
+      const int64_t M = Mof((*cells_)[order_[g0]]);
+      int64_t g1 = g0 + 1;
+      while (g1 < p1 && Mof((*cells_)[order_[g1]]) == M) ++g1;
+      const int iM = (int)M, cnt = (int)(g1 - g0);
+      const int64_t s0 = g0 - p0;
+      rocblas_int* inf = info_.as<rocblas_int>() + g0 * NINFO + which;
+      // info of slot q lands at info_[(g0+q)*NINFO + which]: stride NINFO ints,
+      // so the batched call writes into a contiguous scratch and a copy spreads it
+      rocblas_int* tmp = info_tmp_.as<rocblas_int>();  // chunk_ >= cnt entries
+      const double dM = (double)M;
+      if (which == 0) {
+        sg_.begin(S_EIGH, 4.0 * dM * dM * dM * cnt, 0.0);
+        BC(rocsolver_dsyevd_strided_batched(H_.h, rocblas_evect_original, rocblas_fill_lower, iM,
+                                            Kmm_.as<double>() + s0 * mm, iM, mm,
+                                            eval_.as<double>() + s0 * b_.mmax, b_.mmax,
+                                            E_.as<double>() + s0 * b_.mmax, b_.mmax, tmp, cnt));
+        sg_.end();
+      } else {
+        // L = chol(B); half log-determinants; L^-1 in place (the lanes then form
+        // W' = C L^-T with one GEMM instead of a triangular solve)
+        sg_.begin(S_PANEL, 2.0 * dM * dM * dM / 3 * cnt, 0.0);
+        double* B0 = B_.as<double>() + s0 * mm;
+        BC(rocsolver_dpotrf_strided_batched(H_.h, rocblas_fill_lower, iM, B0, iM, mm, tmp, cnt));
+        hipLaunchKernelGGL(k_nys_logdet, dim3(cnt), dim3(256), 0, st_, B0, M, mm,
+                           stl_.as<double>() + s0 * b_.mmax, b_.mmax,
+                           res_.as<double>() + g0 * NRES, (int64_t)NRES);
+        KC();
+        BC(rocsolver_dtrtri_strided_batched(H_.h, rocblas_fill_lower, rocblas_diagonal_non_unit, iM,
+                                            B0, iM, mm, tmp + cnt, cnt));
+        sg_.end();
+      }
+      HC(hipMemcpy2DAsync(inf, NINFO * sizeof(rocblas_int), tmp, sizeof(rocblas_int),
+                          sizeof(rocblas_int), cnt, hipMemcpyDeviceToDevice, st_));
+      g0 = g1;
+    }
+  }
+
+  struct CellRefs {
+    int64_t c, k, n, M;
+    int in, iM;
+    double dn, dM;
+    const double* x;
+    const double* r;
+    const int64_t* sl;
+    const double* hp;
+    double *sc, *sq, *Kmm, *s, *stl, *C, *B, *rs;
+  };
+  CellRefs refs(int64_t p, int64_t slot) {
+    CellRefs R;
+    R.k = order_[p];
+    R.c = (*cells_)[R.k];
+    R.n = b_.offs[R.c + 1] - b_.offs[R.c];
+    R.M = Mof(R.c);
+    R.in = (int)R.n;
+    R.iM = (int)R.M;
+    R.dn = (double)R.n;
+    R.dM = (double)R.M;
+    R.x = dx_ + b_.offs[R.c] * 3;
+    R.r = dy_ + b_.offs[R.c];
+    R.sl = dsel_.as<int64_t>() + b_.soffs[R.c];
+    R.hp = hyp_ + R.k * 5;
+    const int64_t nmax = b_.nmax, mmax = b_.mmax;
+    R.sc = sc_.as<double>() + slot * nmax * 3;
+    R.sq = sq_.as<double>() + slot * nmax * 3;
+    R.Kmm = Kmm_.as<double>() + slot * mmax * mmax;
+    R.s = eval_.as<double>() + slot * mmax;
+    R.stl = stl_.as<double>() + slot * mmax;
+    R.C = C_.as<double>() + slot * nmax * mmax;
+    R.B = B_.as<double>() + slot * mmax * mmax;
+    R.rs = res_.as<double>() + p * NRES;
+    return R;
+  }
+
+  // scaled inputs, Kmm (NB1 Nystroem: SGPkernel(x[sel]))
+  void phase1(Lane& L, int64_t p, int64_t slot) {
+    const CellRefs R = refs(p, slot);
+    hipStream_t st = L.st;
+    L.sg.begin(S_BUILD, 0.0, 8.0 * R.dM * R.dM);
+    hipLaunchKernelGGL(k_nys_scale, dim3(blocks(R.n, 256)), dim3(256), 0, st, R.x, R.n, R.hp[0],
+                       R.hp[1], R.hp[2], R.sc, obj_ ? R.sq : nullptr);
+    KC();
+    hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.M, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
+                       R.sl, R.M, R.sc, R.sl, R.hp[3], R.Kmm, R.M);
+    KC();
+    L.sg.end();
+  }
+
+  // s clamp, st; Knm = SGPkernel(x, xs=x[sel]); U1 = Knm u; ut, C = Vi ut;
+  // B = diag(1/st) + ut' C
+  void phase3(Lane& L, int64_t p, int64_t slot) {
+    const CellRefs R = refs(p, slot);
+    hipStream_t st = L.st;
+    rocblas_handle h = L.H.h;
+    const double one = 1.0, zero = 0.0;
+    double* Knm = L.Knm.as<double>();
+    double* U1 = L.U1.as<double>();
+    double* ut = L.ut.as<double>();
+    L.sg.begin(S_PANEL, 4 * R.dn * R.dM * R.dM, 8.0 * R.dn * R.dM);
+    hipLaunchKernelGGL(k_nys_eigpost, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.s, R.M, R.n,
+                       R.stl);
+    KC();
+    hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
+                       nullptr, R.n, R.sc, R.sl, R.hp[3], Knm, R.n);
+    KC();
+    BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, R.in, R.iM, R.iM, &one, Knm,
+                     R.in, R.Kmm, R.iM, &zero, U1, R.in));
+    hipLaunchKernelGGL(k_nys_ut, dim3(blocks(R.n * R.M, 256)), dim3(256), 0, st, U1, R.n, R.M, R.s,
+                       std::sqrt(R.dM / R.dn), 1.0 / R.hp[4], ut, R.C);
+    KC();
+    BC(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, R.iM, R.iM, R.in, &one,
+                     ut, R.in, R.C, R.in, &zero, R.B, R.iM));
+    hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.B, R.M, R.M, R.stl, 1,
+                       0.0);
+    KC();
+    L.sg.end();
+  }
+
+  // W' = C L^-T;  A = r/sn2 - W'(W r);  objective (Ki, fused pass);  predict
+  void phase5(Lane& L, int64_t p, int64_t slot) {
+    const CellRefs R = refs(p, slot);
+    hipStream_t st = L.st;
+    rocblas_handle h = L.H.h;
+    const double one = 1.0, zero = 0.0, mone = -1.0;
+    const double sf2 = R.hp[3], isn2 = 1.0 / R.hp[4];
+    const double dn = R.dn, dM = R.dM;
+    double* Wt = L.W.as<double>();  // n x M
+    double* Av = L.Av.as<double>();
+    double* tv = L.tv.as<double>();
+    Stager& sg = L.sg;
+    sg.begin(S_APPLY, 2.0 * dM * dM * dn + 4.0 * dn * dM, 16.0 * dn * dM);
+    hipLaunchKernelGGL(k_nys_zero_upper, dim3(blocks(R.M, 256), (unsigned)R.M), dim3(256), 0, st,
+                       R.B, R.M);
+    KC();
+    BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.iM, R.iM, &one,
+                     R.C, R.in, R.B, R.iM, &zero, Wt, R.in));
+    hipLaunchKernelGGL(k_nys_vi, dim3(blocks(R.n, 256)), dim3(256), 0, st, R.r, R.n, isn2, Av);
+    KC();
+    BC(rocblas_dgemv(h, rocblas_operation_transpose, R.in, R.iM, &one, Wt, R.in, R.r, 1, &zero, tv,
+                     1));
+    BC(rocblas_dgemv(h, rocblas_operation_none, R.in, R.iM, &mone, Wt, R.in, tv, 1, &one, Av, 1));
+    sg.end();
+    if (obj_) {
+      double* Ki = L.Ki.as<double>();
+      sg.begin(S_LOGDET, 2.0 * dn, 16.0 * dn);
+      hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, R.r, Av, R.n, R.rs + 0);
+      KC();
+      sg.end();
+      // Ki = Vi - W'W (full GEMM: rocBLAS dsyrk at this shape is ~2x slower than
+      // dgemm although it does half the flops; the sweep below reads the lower half)
+      sg.begin(S_KI, 2.0 * dn * dn * dM, 8.0 * dn * dn);
+      BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.in, R.iM,
+                       &mone, Wt, R.in, Wt, R.in, &zero, Ki, R.in));
+      hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.n, 256)), dim3(256), 0, st, Ki, R.n, R.n, nullptr,
+                         0, isn2);
+      KC();
+      sg.end();
+      // the lower triangle of Ki read once (~4 n^2 bytes); inputs and A cache-resident
+      sg.begin(S_GRAD, 0.0, 4.0 * dn * dn);
+      const unsigned nt = blocks(R.n, 64);
+      hipLaunchKernelGGL(k_nys_grad, dim3(nt, nt), dim3(256), 0, st, Ki, Av, R.sc, R.sq, R.n, sf2,
+                         L.part.as<double>());
+      KC();
+      hipLaunchKernelGGL(k_nys_partsum, dim3(1), dim3(256), 0, st, L.part.as<double>(),
+                         (int64_t)nt * nt, R.rs + 2);
+      KC();
+      sg.end();
+    }
+    if (pred_) {
+      // k* = SGPkernel(x, xs=xs); fs = mean + k*.A; k*'Ki k* = |k*|^2/sn2 - |W k*|^2
+      sg.begin(S_PRED, 2.0 * dn * dM, 8.0 * dn * dM);
+      double* ks = L.ks.as<double>();
+      double* kv = L.kv.as<double>();
+      hipLaunchKernelGGL(k_nys_scale, dim3(1), dim3(64), 0, st, dxs_.as<double>() + R.c * 3,
+                         (int64_t)1, R.hp[0], R.hp[1], R.hp[2], L.xsc.as<double>(), nullptr);
+      KC();
+      hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), 1), dim3(256), 0, st, R.sc, nullptr,
+                         R.n, L.xsc.as<double>(), nullptr, sf2, ks, R.n);
+      KC();
+      hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, ks, Av, R.n, R.rs + 7);
+      KC();
+      hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, ks, ks, R.n, R.rs + 8);
+      KC();
+      BC(rocblas_dgemv(h, rocblas_operation_transpose, R.in, R.iM, &one, Wt, R.in, ks, 1, &zero, kv,
+                       1));
+      hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, kv, kv, R.M, R.rs + 9);
+      KC();
+      sg.end();
+    }
+  }
+
+  const Batch& b_;
+  hipStream_t st_;
+  bool obj_ = false, pred_ = false, alloc_obj_, alloc_pred_;
+  const double* dx_;
+  const double* dy_;
+  Buf hx_, hy_, dsel_, dxs_, res_, info_;
+  Buf sc_, sq_, Kmm_, eval_, stl_, E_, C_, B_, info_tmp_;
+  int64_t chunk_ = 1;
+  Handle H_;
+  Stager sg_;
+  std::vector<Lane*> lanes_;
+  hipEvent_t ready_ = nullptr;
+  const std::vector<int64_t>* cells_ = nullptr;
+  const double* hyp_ = nullptr;
+  std::vector<int64_t> order_;
+  std::vector<int64_t> cellv_;
+  std::vector<double> hypv_;
+  int64_t ncq_ = 0;
+  double mean_ = 0.0;
+  bool own_ = false;
+  double* hr_ = nullptr;       // pinned: the result copies stay asynchronous
+  rocblas_int* hi_ = nullptr;
+};
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const HipErr& e) {
+    return oi_set_last_error(OI_E_HIP, e.msg.c_str());
+  } catch (const std::bad_alloc&) {
+    return oi_set_last_error(OI_E_NOMEM, "allocation failed");
+  }
+}
 
 }  // namespace
 
@@ -272,204 +857,148 @@ extern "C" int oi_nystrom_batch(const double* xyt, const double* y, const int64_
                                 const double* hyp, const double* xs, double mean, double* nlz,
                                 double* grad, double* pred, int32_t* status,
                                 const oi_options* opts) {
-  if (ncell < 0) return oi_set_last_error(OI_E_ARG, "negative ncell");
+  Batch b{xyt, y, offs, ncell, sel, soffs};
+  if (int rc = check_batch(b)) return rc;
   if (ncell == 0) return 0;
-  if (!offs || !soffs || !sel || !hyp || !xyt || !y || !status)
-    return oi_set_last_error(OI_E_ARG, "null pointer");
-  const bool want_obj = nlz || grad, want_pred = pred != nullptr;
+  if (!hyp || !status) return oi_set_last_error(OI_E_ARG, "null pointer");
   if ((nlz == nullptr) != (grad == nullptr))
     return oi_set_last_error(OI_E_ARG, "nlz and grad go together");
+  const bool want_obj = nlz != nullptr, want_pred = pred != nullptr;
   if (want_pred && !xs) return oi_set_last_error(OI_E_ARG, "pred needs xs");
-  if (offs[0] != 0 || soffs[0] != 0) return oi_set_last_error(OI_E_ARG, "offs[0] must be 0");
-  int64_t nmax = 0, mmax = 0;
-  for (int64_t c = 0; c < ncell; ++c) {
-    const int64_t n = offs[c + 1] - offs[c], M = soffs[c + 1] - soffs[c];
-    if (n < 1 || M < 1 || M > n)
-      return oi_set_last_error(OI_E_ARG, "each cell needs 1 <= M <= n");
-    for (int64_t k = soffs[c]; k < soffs[c + 1]; ++k)
-      if (sel[k] < 0 || sel[k] >= n) return oi_set_last_error(OI_E_ARG, "inducing index out of range");
-    for (int q = 0; q < 5; ++q)
-      if (!(hyp[c * 5 + q] > 0.0)) return oi_set_last_error(OI_E_ARG, "hypers must be > 0");
-    nmax = n > nmax ? n : nmax;
-    mmax = M > mmax ? M : mmax;
-  }
-  if (nmax > INT32_MAX / 2) return oi_set_last_error(OI_E_ARG, "cell too large");
+  for (int64_t q = 0; q < ncell * 5; ++q)
+    if (!(hyp[q] > 0.0)) return oi_set_last_error(OI_E_ARG, "hypers must be > 0");
   oi_options o;
-  oi_options_default(&o);
-  if (opts) o = *opts;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-    return oi_set_last_error(OI_E_NODEV, "no HIP device available");
-  if (o.device < 0 || o.device >= ndev) return oi_set_last_error(OI_E_ARG, "bad device ordinal");
-  if (hipSetDevice(o.device) != hipSuccess) return oi_set_last_error(OI_E_HIP, "hipSetDevice failed");
-  hipStream_t st = (hipStream_t)o.stream;
-  const int64_t N = offs[ncell], S = soffs[ncell];
-  try {
-    Handle H;
-    BC(rocblas_set_stream(H.h, st));
-    // inputs
-    DBuf hx(o.device_inputs ? 0 : N * 3 * sizeof(double));
-    DBuf hy(o.device_inputs ? 0 : N * sizeof(double));
-    const double* dx = xyt;
-    const double* dy = y;
-    if (!o.device_inputs) {
-      HC(hipMemcpyAsync(hx.p, xyt, N * 3 * sizeof(double), hipMemcpyHostToDevice, st));
-      HC(hipMemcpyAsync(hy.p, y, N * sizeof(double), hipMemcpyHostToDevice, st));
-      dx = hx.as<double>();
-      dy = hy.as<double>();
-    }
-    DBuf dsel(S * sizeof(int64_t));
-    HC(hipMemcpyAsync(dsel.p, sel, S * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    DBuf dxs(want_pred ? ncell * 3 * sizeof(double) : 0);
-    if (want_pred) HC(hipMemcpyAsync(dxs.p, xs, ncell * 3 * sizeof(double), hipMemcpyHostToDevice, st));
-    // workspace sized for the largest cell
-    const int64_t nM = nmax * mmax, MM = mmax * mmax;
-    const int64_t ntile = blocks(nmax, 64);
-    DBuf sc(nmax * 3 * 8), sq(nmax * 3 * 8), Kmm(MM * 8), ev(mmax * 8), ew(mmax * 8),
-        stl(mmax * 8), Knm(nM * 8), U1(nM * 8), ut(nM * 8), C(nM * 8), Lt(want_obj ? nM * 8 : 0),
-        B(MM * 8), Hm(want_obj ? MM * 8 : 0), T(nM * 8), Ki(nmax * nmax * 8), Av(nmax * 8),
-        ks(nmax * 8), kv(nmax * 8), xsc(3 * 8), part(ntile * ntile * 5 * 8),
-        res(ncell * NRES * 8), info(ncell * NINFO * sizeof(rocblas_int));
-    HC(hipMemsetAsync(res.p, 0, ncell * NRES * 8, st));
-    HC(hipMemsetAsync(info.p, 0, ncell * NINFO * sizeof(rocblas_int), st));
-    const double one = 1.0, zero = 0.0, mone = -1.0;
+  if (int rc = setup(opts, o)) return rc;
+  return guarded([&] {
+    Runner R(b, o, want_obj, want_pred, xs);
+    std::vector<int64_t> cells(ncell);
+    for (int64_t c = 0; c < ncell; ++c) cells[c] = c;
+    std::vector<CellOut> out(ncell);
+    R.run(cells, hyp, mean, out.data(), want_obj, want_pred);
     for (int64_t c = 0; c < ncell; ++c) {
-      const int64_t n = offs[c + 1] - offs[c], M = soffs[c + 1] - soffs[c];
-      const int in = (int)n, iM = (int)M;
-      const double* x = dx + offs[c] * 3;
-      const double* r = dy + offs[c];
-      const int64_t* sl = dsel.as<int64_t>() + soffs[c];
-      const double* hp = hyp + c * 5;
-      const double sf2 = hp[3], sn2 = hp[4];
-      double* rs = res.as<double>() + c * NRES;
-      rocblas_int* inf = info.as<rocblas_int>() + c * NINFO;
-      hipLaunchKernelGGL(k_nys_scale, dim3(blocks(n, 256)), dim3(256), 0, st, x, n, hp[0], hp[1],
-                         hp[2], sc.as<double>(), want_obj ? sq.as<double>() : nullptr);
-      KC();
-      // Kmm, Knm (NB1 Nystroem: SGPkernel(x[sel]), SGPkernel(x, xs=x[sel]))
-      hipLaunchKernelGGL(k_nys_cross, dim3(blocks(M, 256), (unsigned)M), dim3(256), 0, st,
-                         sc.as<double>(), sl, M, sc.as<double>(), sl, sf2, Kmm.as<double>(), M);
-      KC();
-      hipLaunchKernelGGL(k_nys_cross, dim3(blocks(n, 256), (unsigned)M), dim3(256), 0, st,
-                         sc.as<double>(), nullptr, n, sc.as<double>(), sl, sf2, Knm.as<double>(), n);
-      KC();
-      // s, u = np.linalg.eigh(Kmm)  (LAPACK syevd, lower triangle)
-      BC(rocsolver_dsyevd(H.h, rocblas_evect_original, rocblas_fill_lower, iM, Kmm.as<double>(),
-                          iM, ev.as<double>(), ew.as<double>(), inf + 0));
-      hipLaunchKernelGGL(k_nys_eigpost, dim3(blocks(M, 256)), dim3(256), 0, st, ev.as<double>(), M,
-                         n, stl.as<double>());
-      KC();
-      // U1 = Knm u;  ut, C = Vi ut, Lt
-      BC(rocblas_dgemm(H.h, rocblas_operation_none, rocblas_operation_none, in, iM, iM, &one,
-                       Knm.as<double>(), in, Kmm.as<double>(), iM, &zero, U1.as<double>(), in));
-      hipLaunchKernelGGL(k_nys_ut, dim3(blocks(n * M, 256)), dim3(256), 0, st, U1.as<double>(), n,
-                         M, ev.as<double>(), stl.as<double>(), std::sqrt((double)M / (double)n),
-                         1.0 / sn2, ut.as<double>(), C.as<double>(),
-                         want_obj ? Lt.as<double>() : nullptr);
-      KC();
-      // B = diag(1/st) + ut' Vi ut;  L = chol(B)
-      BC(rocblas_dgemm(H.h, rocblas_operation_transpose, rocblas_operation_none, iM, iM, in, &one,
-                       ut.as<double>(), in, C.as<double>(), in, &zero, B.as<double>(), iM));
-      hipLaunchKernelGGL(k_nys_diag, dim3(blocks(M, 256)), dim3(256), 0, st, B.as<double>(), M, M,
-                         stl.as<double>(), 1, 0.0);
-      KC();
-      BC(rocsolver_dpotrf(H.h, rocblas_fill_lower, iM, B.as<double>(), iM, inf + 1));
-      // alpha = L'^-1 L^-1 (ut' Vi)
-      hipLaunchKernelGGL(k_nys_transpose, dim3(blocks(n, 32), blocks(M, 32)), dim3(32, 8), 0, st,
-                         C.as<double>(), n, M, T.as<double>());
-      KC();
-      BC(rocblas_dtrsm(H.h, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none,
-                       rocblas_diagonal_non_unit, iM, in, &one, B.as<double>(), iM, T.as<double>(),
-                       iM));
-      BC(rocblas_dtrsm(H.h, rocblas_side_left, rocblas_fill_lower, rocblas_operation_transpose,
-                       rocblas_diagonal_non_unit, iM, in, &one, B.as<double>(), iM, T.as<double>(),
-                       iM));
-      // Ki = Vi - Vi ut alpha;  A = Ki r
-      BC(rocblas_dgemm(H.h, rocblas_operation_none, rocblas_operation_none, in, in, iM, &mone,
-                       C.as<double>(), in, T.as<double>(), iM, &zero, Ki.as<double>(), in));
-      hipLaunchKernelGGL(k_nys_diag, dim3(blocks(n, 256)), dim3(256), 0, st, Ki.as<double>(), n, n,
-                         nullptr, 0, 1.0 / sn2);
-      KC();
-      BC(rocblas_dgemv(H.h, rocblas_operation_none, in, in, &one, Ki.as<double>(), in, r, 1, &zero,
-                       Av.as<double>(), 1));
+      status[c] = out[c].status;
       if (want_obj) {
-        hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, r, Av.as<double>(), n, rs + 0);
-        KC();
-        // slogdet(eye(M) sn2 + Lt' Lt) via Cholesky (SPD)
-        BC(rocblas_dgemm(H.h, rocblas_operation_transpose, rocblas_operation_none, iM, iM, in,
-                         &one, Lt.as<double>(), in, Lt.as<double>(), in, &zero, Hm.as<double>(), iM));
-        hipLaunchKernelGGL(k_nys_diag, dim3(blocks(M, 256)), dim3(256), 0, st, Hm.as<double>(), M,
-                           M, nullptr, 0, sn2);
-        KC();
-        BC(rocsolver_dpotrf(H.h, rocblas_fill_lower, iM, Hm.as<double>(), iM, inf + 2));
-        hipLaunchKernelGGL(k_nys_logdiag, dim3(1), dim3(256), 0, st, Hm.as<double>(), M, M, rs + 1);
-        KC();
-        const unsigned nt = blocks(n, 64);
-        hipLaunchKernelGGL(k_nys_grad, dim3(nt, nt), dim3(256), 0, st, Ki.as<double>(),
-                           Av.as<double>(), sc.as<double>(), sq.as<double>(), n, sf2,
-                           part.as<double>());
-        KC();
-        hipLaunchKernelGGL(k_nys_partsum, dim3(1), dim3(256), 0, st, part.as<double>(),
-                           (int64_t)nt * nt, rs + 2);
-        KC();
+        nlz[c] = out[c].nlz;
+        for (int q = 0; q < 5; ++q) grad[c * 5 + q] = out[c].grad[q];
       }
       if (want_pred) {
-        // k* = SGPkernel(x, xs=xs); fs = mean + k*.A; err = k*' Ki k*
-        hipLaunchKernelGGL(k_nys_scale, dim3(1), dim3(64), 0, st, dxs.as<double>() + c * 3,
-                           (int64_t)1, hp[0], hp[1], hp[2], xsc.as<double>(), nullptr);
-        KC();
-        hipLaunchKernelGGL(k_nys_cross, dim3(blocks(n, 256), 1), dim3(256), 0, st, sc.as<double>(),
-                           nullptr, n, xsc.as<double>(), nullptr, sf2, ks.as<double>(), n);
-        KC();
-        hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, ks.as<double>(), Av.as<double>(),
-                           n, rs + 7);
-        KC();
-        BC(rocblas_dgemv(H.h, rocblas_operation_none, in, in, &one, Ki.as<double>(), in,
-                         ks.as<double>(), 1, &zero, kv.as<double>(), 1));
-        hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, ks.as<double>(), kv.as<double>(),
-                           n, rs + 8);
-        KC();
-      }
-    }
-    std::vector<double> hr(ncell * NRES);
-    std::vector<rocblas_int> hi(ncell * NINFO);
-    HC(hipMemcpyAsync(hr.data(), res.p, ncell * NRES * 8, hipMemcpyDeviceToHost, st));
-    HC(hipMemcpyAsync(hi.data(), info.p, ncell * NINFO * sizeof(rocblas_int), hipMemcpyDeviceToHost, st));
-    HC(hipStreamSynchronize(st));
-    const double inf = INFINITY, nan = NAN;
-    for (int64_t c = 0; c < ncell; ++c) {
-      const int64_t n = offs[c + 1] - offs[c];
-      const double sf2 = hyp[c * 5 + 3], sn2 = hyp[c * 5 + 4];
-      const double* rr = hr.data() + c * NRES;
-      const rocblas_int* ii = hi.data() + c * NINFO;
-      // syevd or chol(B) failing is NB1's LinAlgError; chol(H) failing can only
-      // happen on overflow (H = sn2 I + SPD) and is reported the same way
-      const bool bad = ii[0] != 0 || ii[1] != 0 || (want_obj && ii[2] != 0);
-      status[c] = bad ? 1 : 0;
-      if (want_obj) {
-        if (bad) {
-          nlz[c] = inf;
-          for (int q = 0; q < 5; ++q) grad[c * 5 + q] = inf;
-        } else {
-          const double det = (2.0 * rr[1]) / 2.0;
-          nlz[c] = (rr[0] / 2.0 + det) + (double)n * std::log(2.0 * M_PI) / 2.0;
-          grad[c * 5 + 0] = rr[2] / 2.0;
-          grad[c * 5 + 1] = rr[3] / 2.0;
-          grad[c * 5 + 2] = rr[4] / 2.0;
-          grad[c * 5 + 3] = rr[5] / 2.0;
-          grad[c * 5 + 4] = sn2 * rr[6];
-        }
-      }
-      if (want_pred) {
-        pred[c * 3 + 0] = bad ? nan : mean + rr[7];
-        pred[c * 3 + 1] = bad ? nan : std::sqrt(sf2 - rr[8]);
-        pred[c * 3 + 2] = std::sqrt(sf2);
+        pred[c * 3 + 0] = out[c].fs;
+        pred[c * 3 + 1] = out[c].sd;
+        pred[c * 3 + 2] = out[c].sprior;
       }
     }
     return 0;
-  } catch (const HipErr& e) {
-    return oi_set_last_error(OI_E_HIP, e.msg.c_str());
-  } catch (const std::bad_alloc&) {
-    return oi_set_last_error(OI_E_NOMEM, "allocation failed");
-  }
+  });
+}
+
+extern "C" int oi_nystrom_fit_batch(const double* xyt, const double* y, const int64_t* offs,
+                                    int64_t ncell, const int64_t* sel, const int64_t* soffs,
+                                    const double* x0, const double* xs, double mean, double* out,
+                                    int32_t* status, int32_t* info, const oi_options* opts) {
+  Batch b{xyt, y, offs, ncell, sel, soffs};
+  if (int rc = check_batch(b)) return rc;
+  if (ncell == 0) return 0;
+  if (!x0 || !xs || !out || !status) return oi_set_last_error(OI_E_ARG, "null pointer");
+  oi_options o;
+  if (int rc = setup(opts, o)) return rc;
+  // scipy: maxiter = len(x0) * 200 for the notebook's 5 hypers
+  const int32_t maxiter = o.maxiter < 0 ? 1000 : o.maxiter;
+  return guarded([&] {
+    // one restated scipy CG per cell (6-slot; the sixth gradient is 0, which
+    // leaves scipy's iteration unchanged), every round one pass over the cells
+    // still iterating
+    std::vector<oi_cg*> cg(ncell, nullptr);
+    struct Free {
+      std::vector<oi_cg*>& v;
+      ~Free() {
+        for (auto* p : v)
+          if (p) oi_cg_destroy(p);
+      }
+    } free_{cg};
+    double x6[6];
+    for (int q = 0; q < 5; ++q) x6[q] = x0[q];
+    x6[5] = 0.0;
+    std::vector<double> req(ncell * 6);
+    std::vector<char> live(ncell, 0);
+    for (int64_t c = 0; c < ncell; ++c) {
+      cg[c] = oi_cg_create(x6, o.gtol, maxiter);
+      if (!cg[c]) throw std::bad_alloc();
+      const int rc = oi_cg_step(cg[c], req.data() + c * 6);
+      if (rc < 0) throw HipErr{"oi_cg_step failed"};
+      live[c] = rc == 1;
+    }
+    // cells are independent: split them into G groups (OI_NYS_GROUPS, default 2),
+    // each with its own stream and lanes, so one group's latency-bound batched
+    // eigh overlaps the other's panels / objective pass; each group is
+    // collected and re-queued as soon as its round is done
+    int G = 2;
+    if (const char* e = getenv("OI_NYS_GROUPS")) G = atoi(e);
+    G = std::max(1, std::min<int>(G, (int)ncell));
+    std::vector<std::vector<int64_t>> gcells(G);
+    for (int64_t c = 0; c < ncell; ++c) gcells[c % G].push_back(c);
+    std::vector<std::unique_ptr<Runner>> RG;
+    for (int g = 0; g < G; ++g) RG.emplace_back(new Runner(b, o, true, false, xs, G > 1));
+    std::vector<std::vector<int64_t>> qcells(G);
+    std::vector<CellOut> res(ncell);
+    auto queue = [&](int g) {
+      qcells[g].clear();
+      std::vector<double> hyp;
+      for (int64_t c : gcells[g])
+        if (live[c]) {
+          qcells[g].push_back(c);
+          for (int q = 0; q < 5; ++q) hyp.push_back(std::exp(req[c * 6 + q]));  // NB1 SMLII
+        }
+      if (!qcells[g].empty()) RG[g]->enqueue(qcells[g], hyp.data(), mean, true, false);
+    };
+    for (int g = 0; g < G; ++g) queue(g);
+    for (bool any = true; any;) {
+      any = false;
+      for (int g = 0; g < G; ++g) {
+        if (qcells[g].empty()) continue;
+        any = true;
+        RG[g]->collect(res.data());
+        for (size_t k = 0; k < qcells[g].size(); ++k) {
+          const int64_t c = qcells[g][k];
+          const double g6[6] = {res[k].grad[0], res[k].grad[1], res[k].grad[2], res[k].grad[3],
+                                res[k].grad[4], 0.0};
+          if (oi_cg_feed(cg[c], res[k].nlz, g6) != 0) throw HipErr{"oi_cg_feed failed"};
+          const int rc = oi_cg_step(cg[c], req.data() + c * 6);
+          if (rc < 0) throw HipErr{"oi_cg_step failed"};
+          live[c] = rc == 1;
+        }
+        queue(g);
+      }
+    }
+    RG.clear();
+    Runner R(b, o, false, true, xs);
+    std::vector<int64_t> cells;
+    std::vector<double> hyp;
+    // NB1 code cell 5: GPR(approx=True) at the fitted hypers
+    cells.clear();
+    hyp.clear();
+    std::vector<double> xf(ncell * 6);
+    for (int64_t c = 0; c < ncell; ++c) {
+      double fun;
+      int32_t nit, cst;
+      int64_t nfev, njev, nobj;
+      oi_cg_result(cg[c], xf.data() + c * 6, &fun, &nit, &cst, &nfev, &njev, &nobj);
+      if (info) {
+        info[c * 4 + 0] = nit;
+        info[c * 4 + 1] = cst;
+        info[c * 4 + 2] = (int32_t)nfev;
+        info[c * 4 + 3] = (int32_t)nobj;
+      }
+      cells.push_back(c);
+      for (int q = 0; q < 5; ++q) hyp.push_back(std::exp(xf[c * 6 + q]));
+    }
+    R.run(cells, hyp.data(), mean, res.data(), false, true);
+    for (int64_t c = 0; c < ncell; ++c) {
+      status[c] = res[c].status;
+      out[c * 8 + 0] = res[c].fs;
+      out[c * 8 + 1] = res[c].sd;
+      out[c * 8 + 2] = res[c].sprior;
+      for (int q = 0; q < 5; ++q) out[c * 8 + 3 + q] = hyp[c * 5 + q];
+    }
+    return 0;
+  });
 }

@@ -114,61 +114,32 @@ def default_x0(grid_res=25):
                      np.log(.1)])
 
 
-def fit_batch(xyt, y, offs, M, x0=None, gtol=1e-5, maxiter=None):
-    """``minimize(SMLII, x0, args=(x, y, True, M), method='CG', jac=True)`` for
-    every cell at once (NB1 code cell 5): one restated scipy CG per cell on
-    the host, every round one batched GPU objective call over the cells still
-    iterating.  Returns (x [ncell x 5] log-hypers, info list of dicts)."""
-    offs = np.asarray(offs, dtype=np.int64)
-    ncell = len(offs) - 1
-    x0 = default_x0() if x0 is None else np.asarray(x0, dtype=np.float64)
-    # the 5-vector rides in the 6-slot CG with a zero sixth gradient: scipy's
-    # iteration is unchanged by a coordinate whose gradient is 0; maxiter keeps
-    # scipy's len(x0) * 200 for the notebook's 5 hypers
-    maxiter = 200 * 5 if maxiter is None else int(maxiter)
-    sizes = np.diff(offs)
-    Ms = np.broadcast_to(np.asarray(M, dtype=np.int64), sizes.shape)
-    sel, soffs = _ragged_sel(offs, Ms)
-    xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
-    y = np.ascontiguousarray(y, dtype=np.float64)
-    cgs = [_lib.CG(np.append(x0, 0.0), gtol=gtol, maxiter=maxiter) for _ in range(ncell)]
-    want = [cg.step() for cg in cgs]
-    while True:
-        live = [c for c in range(ncell) if want[c] is not None]
-        if not live:
-            break
-        sub_offs = np.zeros(len(live) + 1, dtype=np.int64)
-        sub_offs[1:] = np.cumsum(sizes[live])
-        rows = np.concatenate([np.arange(offs[c], offs[c + 1]) for c in live])
-        s_sel = np.concatenate([sel[soffs[c]:soffs[c + 1]] for c in live])
-        s_offs = np.zeros(len(live) + 1, dtype=np.int64)
-        s_offs[1:] = np.cumsum(Ms[live])
-        h = np.stack([want[c][:5] for c in live])
-        nlz, grad, _, status = _lib.nystrom_batch(xyt[rows], y[rows], sub_offs, s_sel, s_offs,
-                                                  _linear(h), objective=True, predict=False,
-                                                  **options)
-        for k, c in enumerate(live):
-            cgs[c].feed(nlz[k], np.append(grad[k], 0.0))
-            want[c] = cgs[c].step()
-    res = [cg.result() for cg in cgs]
-    return np.stack([r['x'][:5] for r in res]), res
-
-
 def fit_predict_batch(xyt, y, offs, xs, mean, M, x0=None):
-    """NB1 code cell 5 for every cell: fit the hypers on the Nystrom objective,
-    then predict with them.  Returns (pred [ncell x 3], x [ncell x 5], info)."""
-    x, info = fit_batch(xyt, y, offs, M, x0=x0)
+    """NB1 code cell 5 for every cell of a ragged batch in one liboi call
+    (``oi_nystrom_fit_batch``): ``minimize(SMLII, x0, args=(x, y, True, M),
+    method='CG', jac=True)`` per cell -- the restated scipy CG on the host, one
+    GPU pass over the cells still iterating per round -- then
+    ``GPR(approx=True, returnprior=True)`` at the fitted hypers.
+    Returns (pred [ncell x 3] = (fs, sd, prior sd), x [ncell x 5] fitted
+    log-hypers, info [ncell x 4] = (nit, status, nfev, objective evals))."""
+    offs = np.asarray(offs, dtype=np.int64)
     sel, soffs = _ragged_sel(offs, M)
-    _, _, pred, status = _lib.nystrom_batch(xyt, y, offs, sel, soffs, _linear(x), xs=xs,
-                                            mean=mean, objective=False, predict=True, **options)
-    return pred, x, info
+    x0 = default_x0() if x0 is None else np.asarray(x0, dtype=np.float64)
+    out, status, info = _lib.nystrom_fit_batch(xyt, y, offs, sel, soffs, x0, xs, mean, **options)
+    return out[:, :3], np.log(out[:, 3:]), info
 
 
-def fit(x, y, M, x0=None, gtol=1e-5):
-    """One cell of ``fit_batch``: the minimize() result as a dict (x [5], fun,
-    nit, status, nfev, njev, nobj)."""
+def fit_batch(xyt, y, offs, M, x0=None):
+    """The fit half of ``fit_predict_batch``: (x [ncell x 5] log-hypers, info)."""
+    ncell = len(offs) - 1
+    _, x, info = fit_predict_batch(xyt, y, offs, np.zeros((ncell, 3)), 0.0, M, x0=x0)
+    return x, info
+
+
+def fit(x, y, M, x0=None):
+    """One cell of ``fit_batch``: the minimize() result as a dict (x [5], nit,
+    status, nfev, nobj)."""
     y = np.asarray(y, dtype=np.float64).reshape(-1)
-    xh, info = fit_batch(x, y, np.array([0, len(y)]), M, x0=x0, gtol=gtol)
-    r = dict(info[0])
-    r['x'] = xh[0]
-    return r
+    xh, info = fit_batch(x, y, np.array([0, len(y)]), M, x0=x0)
+    return dict(x=xh[0], nit=int(info[0, 0]), status=int(info[0, 1]), nfev=int(info[0, 2]),
+                nobj=int(info[0, 3]))
