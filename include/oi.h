@@ -152,6 +152,32 @@ int oi_nystrom_fit_batch(const double* xyt, const double* y, const int64_t* offs
                          const double* xs, double mean, double* out, int32_t* status,
                          int32_t* info, const oi_options* opts);
 
+/* ---- SVGP variant (dev/sparseGP_example.ipynb code cell 5: GPflow SVGP with a
+ * Matern32 kernel, Gaussian likelihood, Constant mean, whitened q(u), trained
+ * by TF2 Adam on minibatches, then predict_f) -- one workgroup per cell runs
+ * the whole training in one launch --------------------------------------
+ *   xyt [N x 3], y [N]: the cell's inputs and RAW outputs (the Constant mean
+ *       function holds the prior mean, as in the notebook)
+ *   Z0  [ncell x M x 3] initial inducing inputs (NB2: per-dimension linspace)
+ *   init [ncell x 6]: lengthscales (3), kernel variance, noise variance, mean
+ *   batch (<= 256) rows per minibatch, iterations Adam steps (TF2 Adam, lr),
+ *   log_every: the notebook's training_loss() call after every log_every-th
+ *       step (draws one extra minibatch; 0 = none); elbo [ncell x
+ *       ceil(iterations/log_every)] receives those ELBO values (or NULL)
+ *   seed: minibatch stream of cell c keyed by seed + c (a deterministic
+ *       per-epoch permutation; tf.data's shuffle is not reproducible)
+ *   xs [ncell x 3] targets; pred [ncell x 2] = predict_f mean, variance of f
+ *   params [ncell x oi_svgp_param_count(M)] final unconstrained parameters
+ *       (ls_raw[3], var_raw, lik_raw, c, Z[M x 3], q_mu[M], tril(q_sqrt)) or NULL
+ *   status [ncell]: 1 if a K_uu Cholesky failed during training
+ * 1 <= M <= 64. */
+int32_t oi_svgp_param_count(int32_t M);
+int oi_svgp_batch(const double* xyt, const double* y, const int64_t* offs, int64_t ncell,
+                  const double* Z0, int32_t M, const double* init, int32_t batch,
+                  int32_t iterations, int32_t log_every, uint64_t seed, double lr,
+                  const double* xs, double* pred, double* params, double* elbo, int32_t* status,
+                  const oi_options* opts);
+
 /* ---- host optimiser (scipy 1.15 CG restated; see csrc/cg.hpp) ---- */
 typedef struct oi_cg oi_cg;
 /* x0: 6 log-hypers. gtol/maxiter as in oi_options (maxiter < 0 => 1200). */

@@ -35,7 +35,7 @@ EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_cr
            'oi_cg_step', 'oi_cg_feed', 'oi_cg_result', 'oi_cg_destroy', 'oi_last_error',
            'oi_version', 'oi_profile_json', 'oi_profile_reset', 'oi_smooth_fields',
            'oi_ball_query', 'oi_gather_rows', 'oi_nystrom_batch',
-           'oi_nystrom_fit_batch')
+           'oi_nystrom_fit_batch', 'oi_svgp_batch', 'oi_svgp_param_count')
 
 
 class OiOptions(ctypes.Structure):
@@ -109,6 +109,14 @@ def load():
                                              ctypes.c_double, c_double_p, c_int32_p, c_int32_p,
                                              ctypes.POINTER(OiOptions)]
         lib.oi_nystrom_fit_batch.restype = ctypes.c_int
+        lib.oi_svgp_param_count.argtypes = [ctypes.c_int32]
+        lib.oi_svgp_param_count.restype = ctypes.c_int32
+        lib.oi_svgp_batch.argtypes = [c_double_p, c_double_p, c_int64_p, ctypes.c_int64, c_double_p,
+                                      ctypes.c_int32, c_double_p, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_uint64, ctypes.c_double, c_double_p,
+                                      c_double_p, c_double_p, c_double_p, c_int32_p,
+                                      ctypes.POINTER(OiOptions)]
+        lib.oi_svgp_batch.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -289,6 +297,42 @@ def nystrom_fit_batch(xyt, y, offs, sel, soffs, x0, xs, mean, **opt_kw):
                                   _ptr(info, ctypes.c_int32), ctypes.byref(o))
     _check(rc)
     return out, status, info
+
+
+def svgp_batch(xyt, y, offs, Z0, init, xs, batch=100, iterations=10000, log_every=10, seed=0,
+               lr=1e-3, want_params=False, **opt_kw):
+    """oi_svgp_batch: returns (pred [ncell x 2] = (mean, variance of f), status,
+    params [ncell x P] or None, elbo [ncell x nlog] or None).
+    Z0 [ncell x M x 3]; init [ncell x 6] = (ls_x, ls_y, ls_t, kernel var, noise var, mean)."""
+    lib = load()
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    ncell = len(offs) - 1
+    Z0 = np.ascontiguousarray(Z0, dtype=np.float64).reshape(ncell, -1, 3)
+    M = Z0.shape[1]
+    init = np.ascontiguousarray(init, dtype=np.float64).reshape(ncell, 6)
+    xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(ncell, 3)
+    if opt_kw.get('device_inputs'):
+        px, py = _dptr(xyt), _dptr(y)
+    else:
+        xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        if offs[-1] != len(y) or xyt.shape[0] != len(y):
+            raise ValueError("inconsistent ragged batch")
+        px, py = _ptr(xyt, ctypes.c_double), _ptr(y, ctypes.c_double)
+    P = int(lib.oi_svgp_param_count(M))
+    nlog = (iterations + log_every - 1) // log_every if log_every else 0
+    pred = np.empty((ncell, 2))
+    status = np.zeros(ncell, dtype=np.int32)
+    params = np.empty((ncell, P)) if want_params else None
+    elbo = np.empty((ncell, nlog)) if nlog else None
+    o = options(**opt_kw)
+    rc = lib.oi_svgp_batch(px, py, _ptr(offs, ctypes.c_int64), ncell, _ptr(Z0, ctypes.c_double), M,
+                           _ptr(init, ctypes.c_double), int(batch), int(iterations), int(log_every),
+                           int(seed), float(lr), _ptr(xs, ctypes.c_double), _ptr(pred, ctypes.c_double),
+                           _ptr(params, ctypes.c_double), _ptr(elbo, ctypes.c_double),
+                           _ptr(status, ctypes.c_int32), ctypes.byref(o))
+    _check(rc)
+    return pred, status, params, elbo
 
 
 class CG:

@@ -97,3 +97,19 @@ def test_nystrom_argument_errors():
         _lib.nystrom_batch(x, y, [0, 4], np.array([0, 4]), [0, 2], np.ones((1, 5)), predict=False)
     with pytest.raises(_lib.OiError, match='hypers'):
         _lib.nystrom_batch(x, y, [0, 4], np.array([0, 1]), [0, 2], np.zeros((1, 5)), predict=False)
+
+
+def test_svgp_argument_errors():
+    """oi_svgp_batch rejects bad shapes / hypers before any device work."""
+    x = np.zeros((4, 3))
+    y = np.zeros(4)
+    Z = np.zeros((1, 2, 3))
+    ok = [[1.0, 1.0, 1.0, 1.0, 0.1, 0.0]]
+    with pytest.raises(_lib.OiError, match='M must be'):
+        _lib.svgp_batch(x, y, [0, 4], np.zeros((1, 65, 3)), ok, [[0, 0, 0]])
+    with pytest.raises(_lib.OiError, match='batch must be'):
+        _lib.svgp_batch(x, y, [0, 4], Z, ok, [[0, 0, 0]], batch=300)
+    with pytest.raises(_lib.OiError, match='lengthscales'):
+        _lib.svgp_batch(x, y, [0, 4], Z, [[1.0, 0.0, 1.0, 1.0, 0.1, 0.0]], [[0, 0, 0]])
+    with pytest.raises(_lib.OiError, match='n >= 1'):
+        _lib.svgp_batch(x, y, [0, 0, 4], np.zeros((2, 2, 3)), ok * 2, [[0, 0, 0]] * 2)
