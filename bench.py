@@ -22,8 +22,13 @@ observations, M = 925 inducing rows, fit by CG on the Nystrom
 objective + predict (oi_nystrom_fit_batch); weak scaling.  Per rank 32 cells
 (--nys-cells) of n = 4600, M = 925.
 
+`--workload svgp` times the dev notebook's sparse variational GP
+(dev/sparseGP_example.ipynb code cell 5): per rank 256
+cells (--svgp-cells) of n = 4600, M = 50 inducing points (linspace Z), 10 000
+Adam steps on minibatches of 100 + predict_f (oi_svgp_batch, one launch).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-                       [--workload day|dayshard|predict|single|nystrom]
+                       [--workload day|dayshard|predict|single|nystrom|svgp]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -49,9 +54,11 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=1)
     p.add_argument('--warmup', type=int, default=0)
-    p.add_argument('--workload', default='day', choices=['day', 'dayshard', 'predict', 'single', 'nystrom'])
+    p.add_argument('--workload', default='day', choices=['day', 'dayshard', 'predict', 'single', 'nystrom', 'svgp'])
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--nys-cells', type=int, default=0, help='nystrom workload: cells per rank-step')
+    p.add_argument('--svgp-cells', type=int, default=256, help='svgp workload: cells per rank-step')
+    p.add_argument('--svgp-iters', type=int, default=10000, help='svgp workload: Adam steps per cell')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-prime', action='store_true',
                    help='skip the untimed priming call (profiler runs: every dispatch is then a timed one)')
@@ -280,6 +287,121 @@ def main_nystrom(args, torch, dist, world, rank, gpu, cdev):
         dist.destroy_process_group()
 
 
+# ----------------------------------------------------------------- svgp
+SVGP_N, SVGP_M, SVGP_B = 4600, 50, 100
+SVGP_INIT = [25e3, 25e3, 1.0, 1.0, 0.1]  # NB2: lengthscales, kernel variance, noise variance
+
+SVGP_PROBE = r'''
+import os, sys, time, json
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from oracle import svgp_oracle as O
+from optimalinterpolation_amd import synthetic
+n, M, B, steps = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+cells = synthetic.make_cells([n], seed=91)
+x, z, xs = cells.cell(0)
+t = time.perf_counter()
+p, log = O.train(x, z, O.notebook_Z(x, M), [25e3, 25e3, 1.0], 1.0, 0.1, cells.mean, B=B, iterations=steps, seed=1)
+O.predict_f(p, xs)
+print(json.dumps({"steps": steps, "s": time.perf_counter() - t}))
+'''
+
+
+def svgp_cpu_baseline(iters, cores):
+    """The oracle (GPflow SVGP + TF2 Adam restated in NumPy) timed for 300 Adam
+    steps of one cell with single-threaded OpenBLAS, scaled to the workload's
+    steps, ``cores`` such processes in parallel."""
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+    steps = 300
+    out = subprocess.run([sys.executable, '-c', SVGP_PROBE, ROOT, str(SVGP_N), str(SVGP_M), str(SVGP_B),
+                          str(steps)], capture_output=True, text=True, env=env, timeout=600,
+                         check=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    t_cell = r['s'] / steps * iters * 1.1  # + the notebook's logging pass every 10 steps
+    return {"value": cores / t_cell, "unit": "grid-cells/s", "cores": cores, "kind": "port",
+            "sample": (f"oracle/svgp_oracle.py (GPflow SVGP + TF2 Adam restated) timed for {steps} Adam "
+                       f"steps of one n={SVGP_N}, M={SVGP_M}, B={SVGP_B} cell ({r['s']:.2f} s, 1 OpenBLAS "
+                       f"thread), scaled to {iters} steps + 10% logging passes, {cores} such processes "
+                       f"in parallel: extrapolated"), "probe": r}
+
+
+def main_svgp(args, torch, dist, world, rank, gpu, cdev):
+    from optimalinterpolation_amd import _lib, svgp, synthetic
+    dev = torch.device('cuda', gpu)
+    k, iters = args.svgp_cells, args.svgp_iters
+    steps = []
+    for s in range(args.warmup + args.steps):
+        cells = synthetic.make_cells([SVGP_N] * k, seed=args.seed + 1000 * rank + s)
+        Z = np.stack([svgp.notebook_Z(cells.cell(c)[0], SVGP_M) for c in range(k)])
+        init = np.tile(SVGP_INIT + [cells.mean], (k, 1))
+        steps.append((cells, Z, init, torch.from_numpy(cells.xyt).to(dev).contiguous(),
+                      torch.from_numpy(cells.z).to(dev).contiguous()))
+    torch.cuda.synchronize()
+
+    def run(s):
+        cells, Z, init, xd, zd = steps[s]
+        return _lib.svgp_batch(xd, zd, cells.offs, Z, init, cells.xs, batch=SVGP_B, iterations=iters,
+                               log_every=10, seed=s, device=gpu, device_inputs=True, profile=True)
+
+    if not args.no_prime:
+        pc = synthetic.make_cells([300], seed=4321)
+        _lib.svgp_batch(pc.xyt, pc.z, pc.offs, svgp.notebook_Z(pc.xyt, 8)[None], [SVGP_INIT + [pc.mean]],
+                        pc.xs, batch=50, iterations=3, device=gpu)
+    for s in range(args.warmup):
+        run(s)
+    _lib.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = [run(s) for s in range(args.warmup, args.warmup + args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ncells = k * args.steps * world
+    bad = int(sum(int(o[1].sum()) for o in outs))
+    kd = _lib.profile_json()['kernels']['k_svgp_train']  # HIP events around the launch
+    kern_ms = kd['total_ms'] / max(kd['launches'], 1)
+    ach = kd['flops'] / (kd['total_ms'] / 1e3) / 1e12
+    roofline = {"bound": "mfma", "kernel": "k_svgp_train", "achieved": round(ach, 4),
+                "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 5),
+                "traffic": None, "launches": kd['launches'], "avg_launch_ms": round(kern_ms, 3),
+                "flops_per_launch": kd['flops'] / max(kd['launches'], 1),
+                "flop_model": "per Adam step 9 M^2 B + 10/3 M^3 (M=50, B=100) x (steps + logging/3) x cells",
+                "note": "latency-bound per-cell dependency chains (one workgroup per cell); frac is "
+                        "against the fp64 dense peak"}
+    line = {"metric": "grid-cells/sec (SVGP fit+predict, NB2 cell 5), fp64",
+            "value": round(ncells / dt, 4), "unit": "grid-cells/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded cells of the SURVEY §8d generator)",
+            "config": {"workload": f"SVGP (dev/sparseGP_example.ipynb cell 5): {k} cells x n={SVGP_N}, "
+                                   f"M={SVGP_M}, B={SVGP_B}, {iters} Adam steps per rank per step",
+                       "cells_per_step": k * world},
+            "failed_cells": bad, "roofline": roofline}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        try:
+            line["cpu_baseline"] = svgp_cpu_baseline(iters, cores)
+        except Exception as e:
+            line["cpu_baseline"] = {"value": None, "error": repr(e)}
+    else:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, 'w') as f:
+                f.write(s + '\n')
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------- main
 def main():
     args = parse()
@@ -301,6 +423,8 @@ def main():
     cdev = torch.device('cpu') if backend == 'gloo' else dev  # where collective tensors live
     if args.workload == 'nystrom':
         return main_nystrom(args, torch, dist, world, rank, gpu, cdev)
+    if args.workload == 'svgp':
+        return main_svgp(args, torch, dist, world, rank, gpu, cdev)
     from optimalinterpolation_amd import _lib
 
     steps, opt, cfg, scaling = build_steps(args, rank, world)

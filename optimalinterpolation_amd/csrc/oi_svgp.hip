@@ -36,6 +36,8 @@
 #include "../../include/oi.h"
 
 extern "C" int oi_set_last_error(int code, const char* msg);  // oi_engine.cpp
+extern "C" void oi_profile_add(const char* name, int64_t launches, double ms, double flops,
+                               double bytes);  // oi_engine.cpp
 
 namespace {
 
@@ -672,15 +674,38 @@ extern "C" int oi_svgp_batch(const double* xyt, const double* y, const int64_t* 
     const size_t lb = lds_bytes(M, batch, panels);
     HC(hipFuncSetAttribute((const void*)k_svgp_train, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lb));
-    int nt = 256;  // threads per cell (OI_SVGP_THREADS: 64..1024, multiple of 64)
+    // threads per cell (OI_SVGP_THREADS: 64..1024, multiple of 64); 1024 measured
+    // fastest (more waves to hide the latency of the per-step dependency chains)
+    int nt = 1024;
     if (const char* e = getenv("OI_SVGP_THREADS")) nt = atoi(e);
     nt = std::max(64, std::min(NT_MAX, nt / 64 * 64));
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (o.profile) {
+      HC(hipEventCreate(&ev0));
+      HC(hipEventCreate(&ev1));
+      HC(hipEventRecord(ev0, st));
+    }
     hipLaunchKernelGGL(k_svgp_train, dim3((unsigned)ncell), dim3(nt), lb, st, dx, dy,
                        doffs.as<int64_t>(), sh, iterations, log_every, seed, lr, dth.as<double>(),
                        dmom.as<double>(), dg.as<double>(), dsc.as<double>(), dxs.as<double>(),
                        dpred.as<double>(), nlog ? delbo.as<double>() : nullptr, dst.as<int32_t>(),
                        panels ? 1 : 0, dtd.as<unsigned long long>());
     HC(hipGetLastError());
+    if (o.profile) {
+      HC(hipEventRecord(ev1, st));
+      HC(hipEventSynchronize(ev1));
+      float ms = 0.f;
+      HC(hipEventElapsedTime(&ms, ev0, ev1));
+      (void)hipEventDestroy(ev0);
+      (void)hipEventDestroy(ev1);
+      // algorithmic flops per Adam step: the M x M x B products (A, S'A, S SA,
+      // Sbar, Kfbar, Lbar: 4.5 x 2 M^2 B) and M^3 terms (chol, inverse, adjoint:
+      // 5/3 x 2 M^3); logging passes are forward-only (~1/3 of a step)
+      const double dM = M, dB = batch;
+      const double fstep = 9.0 * dM * dM * dB + 10.0 / 3.0 * dM * dM * dM;
+      const double nsteps = iterations + (double)nlog / 3.0;
+      oi_profile_add("k_svgp_train", 1, ms, fstep * nsteps * (double)ncell, 0.0);
+    }
     if (timing) {
       unsigned long long t[16];
       HC(hipMemcpyAsync(t, dtd.p, sizeof(t), hipMemcpyDeviceToHost, st));
