@@ -118,52 +118,94 @@ __device__ inline double m32(const double* a, const double* b, double& e) {
   return (1.0 + SQRT3 * r) * e;
 }
 
-// Cholesky (lower, in place) of the M x M matrix A (ld M) in LDS; false if not PD
-__device__ bool chol_lds(double* A, int M, int* flag) {
+// L = chol(W) for the symmetric M x M matrix W (row-major, LDS; its lower
+// triangle is overwritten).  Right-looking, one barrier per column: in step j
+// every thread reads column j of W (final for this step) and scales it on the
+// fly by 1/sqrt(a_jj) (as LAPACK dpotf2 does), writing L's column j and the
+// trailing lower triangle.  Returns false if a pivot is not positive.
+// (A one-wave variant with lane-owned rows and no block barriers measured 3x
+// slower: each of its ~M^2/2 shuffle + LDS read-modify-write steps is exposed
+// latency.)
+__device__ bool chol_lds(double* W, double* L, int M, int* flag) {
+  const int nt = (int)blockDim.x;
+  for (int e = threadIdx.x; e < M * M; e += nt) L[e] = 0.0;
   if (threadIdx.x == 0) *flag = 0;
   __syncthreads();
   for (int j = 0; j < M; ++j) {
-    if (threadIdx.x == 0) {
-      const double d = A[j * M + j];
-      if (!(d > 0.0)) *flag = 1;
-      A[j * M + j] = sqrt(d);
-    }
-    __syncthreads();
-    const double ljj = A[j * M + j];
-    for (int i = j + 1 + threadIdx.x; i < M; i += (int)blockDim.x) A[i * M + j] /= ljj;
-    __syncthreads();
-    // trailing update of the lower triangle: A[i][k] -= L[i][j] L[k][j], j < k <= i
+    const double d = W[j * M + j];
+    const double ljj = sqrt(d), rj = 1.0 / ljj;
+    if (threadIdx.x == 0 && !(d > 0.0)) *flag = 1;
     const int rem = M - j - 1;
-    for (int e = threadIdx.x; e < rem * rem; e += (int)blockDim.x) {
-      const int i = j + 1 + e / rem, k = j + 1 + e % rem;
-      if (k <= i) A[i * M + k] -= A[i * M + j] * A[k * M + j];
+    for (int e = threadIdx.x; e < rem * rem + rem + 1; e += nt) {
+      if (e < rem * rem) {  // W[i][k] -= l_ij l_kj, j < k <= i
+        const int i = j + 1 + e / rem, k = j + 1 + e % rem;
+        if (k <= i) W[i * M + k] -= (W[i * M + j] * rj) * (W[k * M + j] * rj);
+      } else {  // column j of L
+        const int i = j + (e - rem * rem);
+        L[i * M + j] = i == j ? ljj : W[i * M + j] * rj;
+      }
     }
     __syncthreads();
   }
-  // zero the strict upper triangle
-  for (int e = threadIdx.x; e < M * M; e += (int)blockDim.x)
-    if (e % M > e / M) A[e] = 0.0;
-  __syncthreads();
   return *flag == 0;
 }
 
-// Li = L^-1 (lower), one column per thread (forward substitution)
-__device__ void trinv_lds(const double* L, double* Li, int M) {
-  for (int e = threadIdx.x; e < M * M; e += (int)blockDim.x) Li[e] = 0.0;
+// Li = L^-1 (lower): one wave per column c, lane i holding x_i of the forward
+// substitution L x = e_c (M <= 64); U (M x M scratch) receives L' so the
+// column reads L[i][k] (fixed k, lanes over i) are contiguous
+__device__ void trinv_lds(const double* L, double* Li, double* U, int M) {
+  const int nt = (int)blockDim.x;
+  for (int e = threadIdx.x; e < M * M; e += nt) {
+    U[(e % M) * M + e / M] = L[e];
+    Li[e] = 0.0;
+  }
   __syncthreads();
-  for (int c = threadIdx.x; c < M; c += (int)blockDim.x) {
-    Li[c * M + c] = 1.0 / L[c * M + c];
-    for (int i = c + 1; i < M; ++i) {
-      double s = 0.0;
-      for (int k = c; k < i; ++k) s += L[i * M + k] * Li[k * M + c];
-      Li[i * M + c] = -s / L[i * M + i];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = nt >> 6;
+  for (int c = w; c < M; c += nw) {
+    double x = lane == c ? 1.0 : 0.0;
+    for (int k = c; k < M; ++k) {
+      const double xk = __shfl(x, k, 64) / U[k * M + k];
+      if (lane == k) x = xk;
+      if (lane > k && lane < M) x -= U[k * M + lane] * xk;
     }
+    if (lane >= c && lane < M) Li[lane * M + c] = x;
   }
   __syncthreads();
 }
 
+// Lower-triangle panel product, 4 outputs of one row per thread (one load of
+// P[i][.] feeds 4 independent FMA chains): for j <= i,
+//   f(i, j, sum_b P[i][b] Q[j][b])
+template <class F>
+__device__ inline void tri_pq(const double* P, const double* Q, int M, int B, int LB, F f) {
+  int items = 0;
+  for (int i = 0; i < M; ++i) items += i / 4 + 1;
+  for (int it = threadIdx.x; it < items; it += (int)blockDim.x) {
+    int i = 0, r = it;
+    while (r >= i / 4 + 1) {
+      r -= i / 4 + 1;
+      ++i;
+    }
+    const int j0 = 4 * r, nj = (i - j0 + 1) < 4 ? (i - j0 + 1) : 4;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const double* pi = P + i * LB;
+    const double* q0 = Q + j0 * LB;
+    for (int b = 0; b < B; ++b) {
+      const double pv = pi[b];
+      a0 += pv * q0[b];
+      if (nj > 1) a1 += pv * q0[LB + b];
+      if (nj > 2) a2 += pv * q0[2 * LB + b];
+      if (nj > 3) a3 += pv * q0[3 * LB + b];
+    }
+    f(i, j0, a0);
+    if (nj > 1) f(i, j0 + 1, a1);
+    if (nj > 2) f(i, j0 + 2, a2);
+    if (nj > 3) f(i, j0 + 3, a3);
+  }
+}
+
 struct Shape {
-  int M, B, P, nlog;
+  int M, B, P, nlog, LB;  // LB: panel row stride (B rounded up to odd: fewer LDS bank conflicts)
 };
 
 // parameter vector layout (oracle Params.flat): ls_raw[3], var_raw, lik_raw, c,
@@ -190,23 +232,34 @@ __device__ inline void tmark(Lds& s, int k) {
   }
 }
 
-__host__ __device__ inline size_t carve_doubles(int M, int B, bool panels) {
-  return (size_t)(panels ? 3 * M * M + 2 * M * B : 4 * M * M) + 6 * B + 21 * M + 128 + 17;
+// mode 1: panels in LDS (T3 aliases PA); mode 0: panels in global scratch, T3 in
+// LDS; mode 2 ("lean"): panels and T3 in global scratch (T3 aliases the Abar
+// panel, dead by then) -- the smallest LDS footprint, so two cells share a CU
+__host__ __device__ inline int panel_ld(int B) { return B % 2 ? B : B + 1; }
+
+__host__ __device__ inline size_t carve_doubles(int M, int B, int mode) {
+  const int LB = panel_ld(B);
+  const size_t mats = mode == 1 ? 3 * M * M + 2 * M * LB : (mode == 0 ? 4 * M * M : 3 * M * M);
+  return mats + 6 * B + 21 * M + 128 + 17;
 }
 
-__device__ inline Lds carve(double* base, int M, int B, bool panels) {
+__device__ inline Lds carve(double* base, int M, int B, int mode) {
+  const bool panels = mode == 1;
   Lds s;
   double* p = base;
   s.L = p; p += M * M;
   s.Li = p; p += M * M;
   s.T2 = p; p += M * M;
   if (panels) {
-    s.PA = p; p += M * B;
-    s.P3 = p; p += M * B;
+    s.PA = p; p += M * panel_ld(B);
+    s.P3 = p; p += M * panel_ld(B);
     s.T3 = s.PA;  // M <= B guaranteed by the host
-  } else {
+  } else if (mode == 0) {
     s.PA = s.P3 = nullptr;
     s.T3 = p; p += M * M;
+  } else {
+    s.PA = s.P3 = nullptr;
+    s.T3 = nullptr;  // set to the Abar panel by the kernel
   }
   s.Xb = p; p += B * 3;
   s.yb = p; p += B;
@@ -223,7 +276,7 @@ __device__ inline Lds carve(double* base, int M, int B, bool panels) {
   return s;
 }
 
-inline size_t lds_bytes(int M, int B, bool panels) { return carve_doubles(M, B, panels) * 8 + 16; }
+inline size_t lds_bytes(int M, int B, int mode) { return carve_doubles(M, B, mode) * 8 + 16; }
 constexpr size_t LDS_MAX = 160 * 1024;
 
 // One minibatch: loss (always) and, if grad, the gradient into g[P].
@@ -233,7 +286,7 @@ __device__ double step(const double* __restrict__ th, const double* __restrict__
                        const double* __restrict__ Y, int64_t n, uint64_t seed, int64_t batchno,
                        const Shape& sh, Lds& s, double* __restrict__ X1, double* __restrict__ X2,
                        double* __restrict__ X3, double* __restrict__ g, bool grad, bool* ok) {
-  const int M = sh.M, B = sh.B, tid = threadIdx.x;
+  const int M = sh.M, B = sh.B, LB = sh.LB, tid = threadIdx.x;
   const double ls[3] = {softplus(th[0]), softplus(th[1]), softplus(th[2])};
   const double var = softplus(th[3]), s2 = softplus(th[4]) + LIK_LOWER, c = th[5];
   const double* Z = th + 6;
@@ -252,30 +305,36 @@ __device__ double step(const double* __restrict__ th, const double* __restrict__
   }
   __syncthreads();
   tmark(s, 0);
-  // K_uu + jitter -> L, Cholesky, L^-1
+  // K_uu + jitter -> T2 (working copy), L = chol, Li = L^-1, then S dense -> T2
   for (int e = tid; e < M * M; e += (int)blockDim.x) {
     const int i = e / M, j = e % M;
     double ee;
-    s.L[e] = var * m32(s.Zs + i * 3, s.Zs + j * 3, ee) + (i == j ? JITTER : 0.0);
+    s.T2[e] = var * m32(s.Zs + i * 3, s.Zs + j * 3, ee) + (i == j ? JITTER : 0.0);
   }
   __syncthreads();
   tmark(s, 1);
-  if (!chol_lds(s.L, M, s.flag)) *ok = false;
+  if (!chol_lds(s.T2, s.L, M, s.flag)) *ok = false;
   tmark(s, 2);
-  trinv_lds(s.L, s.Li, M);
+  trinv_lds(s.L, s.Li, s.T2, M);
+  double* Sd = s.T2;  // S (lower, dense) until Lbar overwrites T2
+  for (int e = tid; e < M * M; e += (int)blockDim.x) {
+    const int i = e / M, j = e % M;
+    Sd[e] = j <= i ? St[tri_index(i, j)] : 0.0;
+  }
+  __syncthreads();
   tmark(s, 3);
-  // K_uf -> X1 ; A = Li K_uf -> X2  (row-major M x B)
+  // K_uf -> X1 ; A = Li K_uf -> X2  (row-major M x B, row stride LB)
   for (int e = tid; e < M * B; e += (int)blockDim.x) {
     const int m = e / B, b = e % B;
     double ee;
-    X1[e] = var * m32(s.Zs + m * 3, s.Xb + b * 3, ee);
+    X1[m * LB + b] = var * m32(s.Zs + m * 3, s.Xb + b * 3, ee);
   }
   __syncthreads();
   for (int e = tid; e < M * B; e += (int)blockDim.x) {
     const int m = e / B, b = e % B;
     double a = 0.0;
-    for (int k = 0; k <= m; ++k) a += s.Li[m * M + k] * X1[k * B + b];
-    X2[e] = a;
+    for (int k = 0; k <= m; ++k) a += s.Li[m * M + k] * X1[k * LB + b];
+    X2[m * LB + b] = a;
   }
   __syncthreads();
   tmark(s, 4);
@@ -283,8 +342,8 @@ __device__ double step(const double* __restrict__ th, const double* __restrict__
   for (int e = tid; e < M * B; e += (int)blockDim.x) {
     const int k = e / B, b = e % B;
     double a = 0.0;
-    for (int m = k; m < M; ++m) a += St[tri_index(m, k)] * X2[m * B + b];
-    X3[e] = a;
+    for (int m = k; m < M; ++m) a += Sd[m * M + k] * X2[m * LB + b];
+    X3[k * LB + b] = a;
   }
   __syncthreads();
   // per row: mu, fvar, residual terms
@@ -293,7 +352,7 @@ __device__ double step(const double* __restrict__ th, const double* __restrict__
   for (int b = tid; b < B; b += (int)blockDim.x) {
     double mu = 0.0, aa = 0.0, ss = 0.0;
     for (int m = 0; m < M; ++m) {
-      const double a = X2[m * B + b], sa = X3[m * B + b];
+      const double a = X2[m * LB + b], sa = X3[m * LB + b];
       mu += a * s.q[m];
       aa += a * a;
       ss += sa * sa;
@@ -325,46 +384,41 @@ __device__ double step(const double* __restrict__ th, const double* __restrict__
   for (int e = tid; e < M * B; e += (int)blockDim.x) {
     const int m = e / B, b = e % B;
     double ssa = 0.0;  // (S SA)[m][b] = sum_{k <= m} S[m][k] SA[k][b]
-    for (int k = 0; k <= m; ++k) ssa += St[tri_index(m, k)] * X3[k * B + b];
-    X1[e] = s.q[m] * s.gmu[b] - 2.0 * X2[e] * gv + 2.0 * ssa * gv;
+    for (int k = 0; k <= m; ++k) ssa += Sd[m * M + k] * X3[k * LB + b];
+    X1[m * LB + b] = s.q[m] * s.gmu[b] - 2.0 * X2[m * LB + b] * gv + 2.0 * ssa * gv;
   }
-  for (int m = tid; m < M; m += (int)blockDim.x) {
+  // gq[m] = A[m][.] . gmu + q[m]: 16 lanes per m, shuffle-reduced in fixed order
+  for (int m0 = tid >> 4; m0 < ((M + 3) / 4) * 4; m0 += (int)blockDim.x >> 4) {
+    const int m = m0, part = tid & 15;
     double a = 0.0;
-    for (int b = 0; b < B; ++b) a += X2[m * B + b] * s.gmu[b];
-    s.gq[m] = a + s.q[m];
+    if (m < M)
+      for (int b = part; b < B; b += 16) a += X2[m * LB + b] * s.gmu[b];
+    for (int o = 8; o > 0; o >>= 1) a += __shfl_down(a, o, 16);
+    if (part == 0 && m < M) s.gq[m] = a + s.q[m];
   }
   // Sbar (lower) straight into the gradient: 2 sum_b A[m][b] gv SA[k][b] + S - diag(1/S)
   double* gS = g + 6 + 4 * M;
-  for (int e = tid; e < ntri; e += (int)blockDim.x) {
-    int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) / 2.0);
-    while (tri_index(i, 0) > e) --i;
-    while (tri_index(i + 1, 0) <= e) ++i;
-    const int j = e - tri_index(i, 0);
-    double a = 0.0;
-    for (int b = 0; b < B; ++b) a += X2[i * B + b] * X3[j * B + b];
+  tri_pq(X2, X3, M, B, LB, [&](int i, int j, double a) {
+    const int e = tri_index(i, j);
     double v = 2.0 * gv * a + St[e];
     if (i == j) v -= 1.0 / St[e];
     gS[e] = v;
-  }
+  });
   __syncthreads();
   tmark(s, 6);
   // Kfbar = Li' Abar -> X3 : Kfbar[m][b] = sum_{k >= m} Li[k][m] Abar[k][b]
   for (int e = tid; e < M * B; e += (int)blockDim.x) {
     const int m = e / B, b = e % B;
     double a = 0.0;
-    for (int k = m; k < M; ++k) a += s.Li[k * M + m] * X1[k * B + b];
-    X3[e] = a;
+    for (int k = m; k < M; ++k) a += s.Li[k * M + m] * X1[k * LB + b];
+    X3[m * LB + b] = a;
   }
   __syncthreads();
   tmark(s, 7);
   // Lbar = tril(-Kfbar A') -> T2
-  for (int e = tid; e < M * M; e += (int)blockDim.x) {
-    const int i = e / M, j = e % M;
-    double a = 0.0;
-    if (j <= i)
-      for (int b = 0; b < B; ++b) a += X3[i * B + b] * X2[j * B + b];
-    s.T2[e] = j <= i ? -a : 0.0;
-  }
+  for (int e = tid; e < M * M; e += (int)blockDim.x)
+    if (e % M > e / M) s.T2[e] = 0.0;
+  tri_pq(X3, X2, M, B, LB, [&](int i, int j, double a) { s.T2[i * M + j] = -a; });
   __syncthreads();
   tmark(s, 8);
   // P = Phi(L' Lbar) -> T3 : P[i][j] = sum_{k >= i} L[k][i] Lbar[k][j], i >= j, diag / 2
@@ -409,7 +463,7 @@ __device__ double step(const double* __restrict__ th, const double* __restrict__
       for (int b = part4; b < B; b += nparts) {
         double e;
         const double kk = var * m32(zm, s.Xb + b * 3, e);
-        const double kb = X3[m * B + b];
+        const double kb = X3[m * LB + b];
         const double W = kb * (-1.5 * var) * e;
         acc[0] += kb * kk / var;
         for (int d = 0; d < 3; ++d) {
@@ -478,13 +532,14 @@ __device__ void predict(const double* __restrict__ th, const double* xs, const S
   for (int e = tid; e < M * M; e += (int)blockDim.x) {
     const int i = e / M, j = e % M;
     double ee;
-    s.L[e] = var * m32(s.Zs + i * 3, s.Zs + j * 3, ee) + (i == j ? JITTER : 0.0);
+    s.T2[e] = var * m32(s.Zs + i * 3, s.Zs + j * 3, ee) + (i == j ? JITTER : 0.0);
   }
   __syncthreads();
-  if (!chol_lds(s.L, M, s.flag)) *ok = false;
+  if (!chol_lds(s.T2, s.L, M, s.flag)) *ok = false;
+  __syncthreads();
   // k_us -> T2[0..M) ; a = L^-1 k_us -> T3[0..M) by forward substitution (thread 0; M small)
   double* ku = s.T2;
-  double* av = s.T3;
+  double* av = s.Li;
   for (int m = tid; m < M; m += (int)blockDim.x) {
     double ee;
     ku[m] = var * m32(s.Zs + m * 3, s.Xb, ee);
@@ -522,7 +577,7 @@ __global__ void __launch_bounds__(NT_MAX) k_svgp_train(
   extern __shared__ double lds[];
   const int64_t c = blockIdx.x;
   const int M = sh.M, B = sh.B, P = sh.P, tid = threadIdx.x;
-  Lds s = carve(lds, M, B, panels != 0);
+  Lds s = carve(lds, M, B, panels);
   const int64_t n = offs[c + 1] - offs[c];
   const double* X = xyt + offs[c] * 3;
   const double* Y = y + offs[c];
@@ -530,9 +585,11 @@ __global__ void __launch_bounds__(NT_MAX) k_svgp_train(
   double* m1 = mom + c * 2 * P;
   double* m2 = m1 + P;
   double* g = grad + c * P;
-  double* X1 = scratch + c * 3 * (int64_t)M * B;
-  double* X2 = panels ? s.PA : X1 + (int64_t)M * B;
-  double* X3 = panels ? s.P3 : X1 + 2 * (int64_t)M * B;
+  const int64_t pan = (int64_t)M * sh.LB;
+  double* X1 = scratch + c * 3 * pan;
+  double* X2 = panels == 1 ? s.PA : X1 + pan;
+  double* X3 = panels == 1 ? s.P3 : X1 + 2 * pan;
+  if (panels == 2) s.T3 = X1;  // M <= B guaranteed by the host
   const uint64_t cseed = seed + (uint64_t)c;
   bool ok = true;
   if (tid < 17) s.tacc[tid] = 0;
@@ -649,7 +706,7 @@ extern "C" int oi_svgp_batch(const double* xyt, const double* y, const int64_t* 
       for (int i = 0; i < M; ++i) t[6 + 4 * M + i * (i + 1) / 2 + i] = 1.0;
     }
     Buf dth((size_t)ncell * P * 8), dmom((size_t)ncell * 2 * P * 8), dg((size_t)ncell * P * 8),
-        dsc((size_t)ncell * 3 * M * batch * 8), dxs((size_t)ncell * 3 * 8), dpred((size_t)ncell * 2 * 8),
+        dsc((size_t)ncell * 3 * M * panel_ld(batch) * 8), dxs((size_t)ncell * 3 * 8), dpred((size_t)ncell * 2 * 8),
         delbo((size_t)ncell * (nlog ? nlog : 1) * 8), dst((size_t)ncell * 4), doffs((ncell + 1) * 8);
     Buf hx(o.device_inputs ? 0 : N * 3 * 8), hy(o.device_inputs ? 0 : N * 8);
     const double* dx = xyt;
@@ -664,13 +721,17 @@ extern "C" int oi_svgp_batch(const double* xyt, const double* y, const int64_t* 
     HC(hipMemsetAsync(dmom.p, 0, (size_t)ncell * 2 * P * 8, st));
     HC(hipMemcpyAsync(dxs.p, xs, ncell * 3 * 8, hipMemcpyHostToDevice, st));
     HC(hipMemcpyAsync(doffs.p, offs, (ncell + 1) * 8, hipMemcpyHostToDevice, st));
-    Shape sh{M, batch, P, nlog};
+    Shape sh{M, batch, P, nlog, panel_ld(batch)};
     const bool timing = getenv("OI_SVGP_TIMING") && atoi(getenv("OI_SVGP_TIMING")) != 0;
     Buf dtd(timing ? 16 * 8 : 0);
     if (timing) HC(hipMemsetAsync(dtd.p, 0, 16 * 8, st));
-    // panels in LDS when they fit (OI_SVGP_PANELS=0 forces the global scratch)
-    bool panels = M <= batch && lds_bytes(M, batch, true) <= LDS_MAX;
-    if (const char* e = getenv("OI_SVGP_PANELS")) panels = panels && atoi(e) != 0;
+    // LDS layout mode (see carve): 1 when the panels fit, else 0; OI_SVGP_PANELS
+    // overrides (0 / 1 / 2), falling back to 0 where the request cannot hold
+    int panels = (M <= batch && lds_bytes(M, batch, 1) <= LDS_MAX) ? 1 : 0;
+    if (const char* e = getenv("OI_SVGP_PANELS")) {
+      const int want = atoi(e);
+      panels = (want == 1 && panels == 1) ? 1 : ((want == 2 && M <= batch) ? 2 : 0);
+    }
     const size_t lb = lds_bytes(M, batch, panels);
     HC(hipFuncSetAttribute((const void*)k_svgp_train, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lb));
@@ -689,7 +750,7 @@ extern "C" int oi_svgp_batch(const double* xyt, const double* y, const int64_t* 
                        doffs.as<int64_t>(), sh, iterations, log_every, seed, lr, dth.as<double>(),
                        dmom.as<double>(), dg.as<double>(), dsc.as<double>(), dxs.as<double>(),
                        dpred.as<double>(), nlog ? delbo.as<double>() : nullptr, dst.as<int32_t>(),
-                       panels ? 1 : 0, dtd.as<unsigned long long>());
+                       panels, dtd.as<unsigned long long>());
     HC(hipGetLastError());
     if (o.profile) {
       HC(hipEventRecord(ev1, st));
@@ -710,7 +771,7 @@ extern "C" int oi_svgp_batch(const double* xyt, const double* y, const int64_t* 
       unsigned long long t[16];
       HC(hipMemcpyAsync(t, dtd.p, sizeof(t), hipMemcpyDeviceToHost, st));
       HC(hipStreamSynchronize(st));
-      fprintf(stderr, "svgp phase cycles (cell 0, threads %d, panels %d):", nt, (int)panels);
+      fprintf(stderr, "svgp phase cycles (cell 0, threads %d, mode %d):", nt, panels);
       for (int k = 0; k < 13; ++k) fprintf(stderr, " %d:%llu", k, t[k]);
       fprintf(stderr, "\n");
     }
