@@ -91,11 +91,16 @@ __global__ void k_nys_cross(const double* __restrict__ sa, const int64_t* __rest
   out[i + ld * j] = sf2 * ((1.0 + Q) * exp(-Q));
 }
 
-// s[s <= 0] = 1e-12; st = n * s / M
-__global__ void k_nys_eigpost(double* __restrict__ s, int64_t M, int64_t n,
+// s[s <= 0] = 1e-12; st = n * s / M  for the M real eigenvalues; st = 1 on a
+// padded tail (so the pad contributes log 1 = 0 to the batched log-determinant)
+__global__ void k_nys_eigpost(double* __restrict__ s, int64_t M, int64_t Mp, int64_t n,
                               double* __restrict__ st) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= M) return;
+  if (k >= Mp) return;
+  if (k >= M) {
+    st[k] = 1.0;
+    return;
+  }
   double v = s[k];
   if (v <= 0.0) v = 1e-12;
   s[k] = v;
@@ -158,7 +163,8 @@ __global__ void __launch_bounds__(256) k_nys_dot(const double* __restrict__ a,
 //   res[b * NRES_ + 1] = sum_k log L_b[k + M k] + (sum_k log st_b[k]) / 2
 // (slogdet(H)/2 minus M log(sn2)/2; one block per matrix)
 __global__ void __launch_bounds__(256) k_nys_logdet(const double* __restrict__ L, int64_t M,
-                                                    int64_t strideL, const double* __restrict__ st,
+                                                    int64_t ld, int64_t strideL,
+                                                    const double* __restrict__ st,
                                                     int64_t strideS, double* __restrict__ res,
                                                     int64_t strideR) {
   __shared__ double red[8];
@@ -167,18 +173,29 @@ __global__ void __launch_bounds__(256) k_nys_logdet(const double* __restrict__ L
   st += b * strideS;
   double v[2] = {0.0, 0.0};
   for (int64_t i = threadIdx.x; i < M; i += 256) {
-    v[0] += log(L[i + M * i]);
+    v[0] += log(L[i + ld * i]);
     v[1] += log(st[i]);
   }
   block_sum<2>(v, red);
   if (threadIdx.x == 0) res[b * strideR + 1] = v[0] + v[1] / 2.0;
 }
 
-// zero the strict upper triangle of a column-major M x M matrix (potrf / trtri
-// leave the caller's upper triangle in place)
-__global__ void k_nys_zero_upper(double* __restrict__ A, int64_t M) {
+// zero the strict upper triangle of a column-major M x M matrix (leading
+// dimension ld; potrf / trtri leave the caller's upper triangle in place)
+__global__ void k_nys_zero_upper(double* __restrict__ A, int64_t M, int64_t ld) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
-  if (i < j) A[i + M * j] = 0.0;
+  if (i < j && j < M) A[i + ld * j] = 0.0;
+}
+
+// pad the M x M matrix in the top-left of an Mp x Mp column-major buffer to a
+// block-diagonal diag(A, d I): rows / columns M..Mp-1 zero except d on the
+// diagonal.  Householder tridiagonalisation and Cholesky never mix the two
+// blocks (the reflectors' entries in the pad rows are exactly 0), so the
+// leading block's factors and eigenpairs are those of A itself.
+__global__ void k_nys_pad(double* __restrict__ A, int64_t M, int64_t Mp, double d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+  if (i >= Mp || (i < M && j < M)) return;
+  A[i + Mp * j] = i == j ? d : 0.0;
 }
 
 // The objective's n x n pass (NB1 SMLII, approx branch): the five sums
@@ -484,9 +501,15 @@ class Runner {
     nl = nl > b.ncell ? (int)b.ncell : nl;
     for (int l = 0; l < nl; ++l)
       lanes_.emplace_back(new Lane(b.nmax, b.mmax, want_obj, want_pred, o.profile != 0));
-    // slot arrays: sc, sq (n x 3), Kmm (M^2), s, st, E (M), C (n x M), B (M^2);
+    // padding quantum for the batched factorisations (OI_NYS_PAD, default 32;
+    // 0 = batch only cells of equal M): K_mm and B of a cell are factored as
+    // diag(A, d I) of size Mp = M rounded up, so cells of different M share
+    // one strided-batched call
+    if (const char* e = getenv("OI_NYS_PAD")) padq_ = std::max(0, atoi(e));
+    mpmax_ = Mp(b.mmax);
+    // slot arrays: sc, sq (n x 3), Kmm (Mp^2), s, st, E (Mp), C (n x M), B (Mp^2);
     // chunk <= 64 cells and <= 1/4 of the free HBM
-    const int64_t nmax = b.nmax, mmax = b.mmax;
+    const int64_t nmax = b.nmax, mmax = mpmax_;
     const size_t per = (size_t)(6 * nmax + 2 * mmax * mmax + 3 * mmax + nmax * mmax) * 8;
     size_t fr = 0, tot = 0;
     HC(hipMemGetInfo(&fr, &tot));
@@ -601,6 +624,7 @@ class Runner {
 
  private:
   int64_t Mof(int64_t c) const { return b_.soffs[c + 1] - b_.soffs[c]; }
+  int64_t Mp(int64_t M) const { return padq_ > 0 ? (M + padq_ - 1) / padq_ * padq_ : M; }
 
   // per-cell phase `ph` for positions [p0, p1) dealt over the lanes, fenced
   // against the main stream on both sides
@@ -621,13 +645,13 @@ class Runner {
   }
 
   // which = 0: s, u = eigh(Kmm) (syevd); 1: L = chol(B) (potrf) -- one
-  // strided-batched call per equal-M run of slots, on the main stream
+  // strided-batched call per run of slots with equal padded size, on the main stream
   void batched(int64_t p0, int64_t p1, int which) {
-    const int64_t mm = b_.mmax * b_.mmax;
+    const int64_t mm = mpmax_ * mpmax_;
     for (int64_t g0 = p0; g0 < p1;) {
-      const int64_t M = Mof((*cells_)[order_[g0]]);
+      const int64_t M = Mp(Mof((*cells_)[order_[g0]]));  // padded size of the group
       int64_t g1 = g0 + 1;
-      while (g1 < p1 && Mof((*cells_)[order_[g1]]) == M) ++g1;
+      while (g1 < p1 && Mp(Mof((*cells_)[order_[g1]])) == M) ++g1;
       const int iM = (int)M, cnt = (int)(g1 - g0);
       const int64_t s0 = g0 - p0;
       rocblas_int* inf = info_.as<rocblas_int>() + g0 * NINFO + which;
@@ -639,8 +663,8 @@ class Runner {
         sg_.begin(S_EIGH, 4.0 * dM * dM * dM * cnt, 0.0);
         BC(rocsolver_dsyevd_strided_batched(H_.h, rocblas_evect_original, rocblas_fill_lower, iM,
                                             Kmm_.as<double>() + s0 * mm, iM, mm,
-                                            eval_.as<double>() + s0 * b_.mmax, b_.mmax,
-                                            E_.as<double>() + s0 * b_.mmax, b_.mmax, tmp, cnt));
+                                            eval_.as<double>() + s0 * mpmax_, mpmax_,
+                                            E_.as<double>() + s0 * mpmax_, mpmax_, tmp, cnt));
         sg_.end();
       } else {
         // L = chol(B); half log-determinants; L^-1 in place (the lanes then form
@@ -648,8 +672,9 @@ class Runner {
         sg_.begin(S_PANEL, 2.0 * dM * dM * dM / 3 * cnt, 0.0);
         double* B0 = B_.as<double>() + s0 * mm;
         BC(rocsolver_dpotrf_strided_batched(H_.h, rocblas_fill_lower, iM, B0, iM, mm, tmp, cnt));
-        hipLaunchKernelGGL(k_nys_logdet, dim3(cnt), dim3(256), 0, st_, B0, M, mm,
-                           stl_.as<double>() + s0 * b_.mmax, b_.mmax,
+        // the pad block is the identity: log 1 = 0 and st is 1 there (see phase3)
+        hipLaunchKernelGGL(k_nys_logdet, dim3(cnt), dim3(256), 0, st_, B0, M, M, mm,
+                           stl_.as<double>() + s0 * mpmax_, mpmax_,
                            res_.as<double>() + g0 * NRES, (int64_t)NRES);
         KC();
         BC(rocsolver_dtrtri_strided_batched(H_.h, rocblas_fill_lower, rocblas_diagonal_non_unit, iM,
@@ -663,8 +688,8 @@ class Runner {
   }
 
   struct CellRefs {
-    int64_t c, k, n, M;
-    int in, iM;
+    int64_t c, k, n, M, Mp;
+    int in, iM, iMp;
     double dn, dM;
     const double* x;
     const double* r;
@@ -678,15 +703,17 @@ class Runner {
     R.c = (*cells_)[R.k];
     R.n = b_.offs[R.c + 1] - b_.offs[R.c];
     R.M = Mof(R.c);
+    R.Mp = Mp(R.M);
     R.in = (int)R.n;
     R.iM = (int)R.M;
+    R.iMp = (int)R.Mp;
     R.dn = (double)R.n;
     R.dM = (double)R.M;
     R.x = dx_ + b_.offs[R.c] * 3;
     R.r = dy_ + b_.offs[R.c];
     R.sl = dsel_.as<int64_t>() + b_.soffs[R.c];
     R.hp = hyp_ + R.k * 5;
-    const int64_t nmax = b_.nmax, mmax = b_.mmax;
+    const int64_t nmax = b_.nmax, mmax = mpmax_;
     R.sc = sc_.as<double>() + slot * nmax * 3;
     R.sq = sq_.as<double>() + slot * nmax * 3;
     R.Kmm = Kmm_.as<double>() + slot * mmax * mmax;
@@ -707,8 +734,15 @@ class Runner {
                        R.hp[1], R.hp[2], R.sc, obj_ ? R.sq : nullptr);
     KC();
     hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.M, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
-                       R.sl, R.M, R.sc, R.sl, R.hp[3], R.Kmm, R.M);
+                       R.sl, R.M, R.sc, R.sl, R.hp[3], R.Kmm, R.Mp);
     KC();
+    if (R.Mp > R.M) {
+      // pad eigenvalue above every eigenvalue of K_mm (<= trace = M sf2), so the
+      // M real eigenpairs stay first in syevd's ascending order
+      hipLaunchKernelGGL(k_nys_pad, dim3(blocks(R.Mp, 256), (unsigned)R.Mp), dim3(256), 0, st,
+                         R.Kmm, R.M, R.Mp, 2.0 * R.dM * R.hp[3] + 1.0);
+      KC();
+    }
     L.sg.end();
   }
 
@@ -723,22 +757,27 @@ class Runner {
     double* U1 = L.U1.as<double>();
     double* ut = L.ut.as<double>();
     L.sg.begin(S_PANEL, 4 * R.dn * R.dM * R.dM, 8.0 * R.dn * R.dM);
-    hipLaunchKernelGGL(k_nys_eigpost, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.s, R.M, R.n,
-                       R.stl);
+    hipLaunchKernelGGL(k_nys_eigpost, dim3(blocks(R.Mp, 256)), dim3(256), 0, st, R.s, R.M, R.Mp,
+                       R.n, R.stl);
     KC();
     hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
                        nullptr, R.n, R.sc, R.sl, R.hp[3], Knm, R.n);
     KC();
     BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, R.in, R.iM, R.iM, &one, Knm,
-                     R.in, R.Kmm, R.iM, &zero, U1, R.in));
+                     R.in, R.Kmm, R.iMp, &zero, U1, R.in));
     hipLaunchKernelGGL(k_nys_ut, dim3(blocks(R.n * R.M, 256)), dim3(256), 0, st, U1, R.n, R.M, R.s,
                        std::sqrt(R.dM / R.dn), 1.0 / R.hp[4], ut, R.C);
     KC();
     BC(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, R.iM, R.iM, R.in, &one,
-                     ut, R.in, R.C, R.in, &zero, R.B, R.iM));
-    hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.B, R.M, R.M, R.stl, 1,
+                     ut, R.in, R.C, R.in, &zero, R.B, R.iMp));
+    hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.B, R.M, R.Mp, R.stl, 1,
                        0.0);
     KC();
+    if (R.Mp > R.M) {
+      hipLaunchKernelGGL(k_nys_pad, dim3(blocks(R.Mp, 256), (unsigned)R.Mp), dim3(256), 0, st, R.B,
+                         R.M, R.Mp, 1.0);
+      KC();
+    }
     L.sg.end();
   }
 
@@ -756,10 +795,10 @@ class Runner {
     Stager& sg = L.sg;
     sg.begin(S_APPLY, 2.0 * dM * dM * dn + 4.0 * dn * dM, 16.0 * dn * dM);
     hipLaunchKernelGGL(k_nys_zero_upper, dim3(blocks(R.M, 256), (unsigned)R.M), dim3(256), 0, st,
-                       R.B, R.M);
+                       R.B, R.M, R.Mp);
     KC();
     BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.iM, R.iM, &one,
-                     R.C, R.in, R.B, R.iM, &zero, Wt, R.in));
+                     R.C, R.in, R.B, R.iMp, &zero, Wt, R.in));
     hipLaunchKernelGGL(k_nys_vi, dim3(blocks(R.n, 256)), dim3(256), 0, st, R.r, R.n, isn2, Av);
     KC();
     BC(rocblas_dgemv(h, rocblas_operation_transpose, R.in, R.iM, &one, Wt, R.in, R.r, 1, &zero, tv,
@@ -823,6 +862,8 @@ class Runner {
   Buf hx_, hy_, dsel_, dxs_, res_, info_;
   Buf sc_, sq_, Kmm_, eval_, stl_, E_, C_, B_, info_tmp_;
   int64_t chunk_ = 1;
+  int padq_ = 32;
+  int64_t mpmax_ = 0;
   Handle H_;
   Stager sg_;
   std::vector<Lane*> lanes_;
