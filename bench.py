@@ -368,9 +368,18 @@ def main_svgp(args, torch, dist, world, rank, gpu, cdev):
     kd = _lib.profile_json()['kernels']['k_svgp_train']  # HIP events around the launch
     kern_ms = kd['total_ms'] / max(kd['launches'], 1)
     ach = kd['flops'] / (kd['total_ms'] / 1e3) / 1e12
+    traffic = None
+    tfile = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(tfile) and k == 256 and iters == 10000:  # measured for the default shape
+        traffic = json.load(open(tfile)).get('k_svgp_train', {}).get('hbm_bytes_per_launch')
     roofline = {"bound": "mfma", "kernel": "k_svgp_train", "achieved": round(ach, 4),
                 "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 5),
-                "traffic": None, "launches": kd['launches'], "avg_launch_ms": round(kern_ms, 3),
+                "traffic": traffic,
+                "traffic_note": ("HBM bytes per launch, rocprofv3 PMC FETCH_SIZE(x2)+WRITE_SIZE, "
+                                 "profiles/r01/pmc_hbm_bytes_svgp.json: parameters / Adam moments / "
+                                 "K_uf panels re-read from L2 misses, ~3.5 % of HBM bandwidth")
+                if traffic else None,
+                "launches": kd['launches'], "avg_launch_ms": round(kern_ms, 3),
                 "flops_per_launch": kd['flops'] / max(kd['launches'], 1),
                 "flop_model": "per Adam step 9 M^2 B + 10/3 M^3 (M=50, B=100) x (steps + logging/3) x cells",
                 "note": "latency-bound per-cell dependency chains (one workgroup per cell); frac is "

@@ -14,7 +14,10 @@ def load(d, counter):
             for row in csv.DictReader(fh):
                 if row.get('Counter_Name') != counter:
                     continue
-                k = row['Kernel_Name'].split('(')[0]
+                name = row['Kernel_Name']
+                if name.startswith('(anonymous namespace)::'):
+                    name = name[len('(anonymous namespace)::'):]
+                k = name.split('(')[0]
                 per[k][row['Dispatch_Id']] += float(row['Counter_Value'])
     return per
 
