@@ -45,6 +45,7 @@
 #include <vector>
 
 #include "../../include/oi.h"
+#include "oi_gemm.h"
 
 #pragma clang fp contract(off)
 
@@ -257,6 +258,84 @@ __global__ void __launch_bounds__(256) k_nys_partsum(const double* __restrict__ 
     for (int q = 0; q < 5; ++q) out[q] = v[q];
 }
 
+// W' (n x M, column-major) -> 64 x 64 k-major tiles Wp[kt][it] (element
+// kk*64 + mm = W'[64 it + mm][64 kt + kk], zero beyond n / M): the operand
+// layout of the MFMA tile GEMM core (oi_gemm.h)
+__global__ void __launch_bounds__(256) k_nys_pack(const double* __restrict__ Wt, int64_t n,
+                                                  int64_t M, int Tn, double* __restrict__ Wp) {
+  const int it = blockIdx.x % Tn, kt = blockIdx.x / Tn;
+  double* dst = Wp + (size_t)blockIdx.x * 4096;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int64_t a = (int64_t)it * 64 + (e & 63), k = (int64_t)kt * 64 + (e >> 6);
+    dst[e] = (a < n && k < M) ? Wt[a + n * k] : 0.0;
+  }
+}
+
+// The objective's n x n pass without materialising Ki: per lower 64 x 64 tile
+// (i >= j) the MFMA core forms (W'W)_ij = sum_k Wp[k][i]^T Wp[k][j] in
+// registers, then Ki = [a == b]/sn2 - (W'W)_ab, Q = Ki - A_a A_b and the five
+// sums against K, dK regenerated from the scaled inputs (as k_nys_grad),
+// off-diagonal entries weighted 2.  One partial row of 5 per tile.
+__global__ void __launch_bounds__(256) k_nys_grad_mfma(const double* __restrict__ Wp, int Tn,
+                                                       int Tk, const double* __restrict__ A,
+                                                       const double* __restrict__ sc,
+                                                       const double* __restrict__ sq, int64_t n,
+                                                       double sf2, double isn2,
+                                                       double* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
+  const int tile = blockIdx.x;
+  int i = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+  while ((i + 1) * (i + 2) / 2 <= tile) ++i;
+  while (i * (i + 1) / 2 > tile) --i;
+  const int j = tile - i * (i + 1) / 2;
+  Quad acc;
+  quad_zero(acc);
+  gemm1_kmajor(acc, lds, Tk, [&](int p, const double*& a, const double*& b) {
+    a = Wp + ((size_t)p * Tn + i) * 4096;
+    b = Wp + ((size_t)p * Tn + j) * 4096;
+  });
+  double* cQ = lds;            // [3][128] scaled inputs (distance), rows i | columns j
+  double* cq = lds + 3 * 128;  // [3][128] per-dimension scaled inputs
+  double* al = lds + 6 * 128;  // [128] A
+  double* red = lds + 7 * 128;
+  const int t = threadIdx.x;
+  if (t < 128) {
+    const int64_t a = t < 64 ? (int64_t)i * 64 + t : (int64_t)j * 64 + (t - 64);
+    for (int d = 0; d < 3; ++d) {
+      cQ[d * 128 + t] = a < n ? sc[3 * a + d] : 0.0;
+      cq[d * 128 + t] = a < n ? sq[3 * a + d] : 0.0;
+    }
+    al[t] = a < n ? A[a] : 0.0;
+  }
+  __syncthreads();
+  double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb)
+      for (int r = 0; r < 4; ++r) {
+        const int m = acc1_row(mb, r), nn = acc1_col(nb);
+        const int64_t a = (int64_t)i * 64 + m, b = (int64_t)j * 64 + nn;
+        if (a >= n || b >= n || (i == j && m < nn)) continue;
+        const double x = acc.c[mb][nb][r];
+        const double Ki = a == b ? isn2 - x : -x;
+        const double Q = Ki - al[m] * al[64 + nn];
+        const double d0 = cQ[m] - cQ[64 + nn], d1 = cQ[128 + m] - cQ[128 + 64 + nn],
+                     d2 = cQ[256 + m] - cQ[256 + 64 + nn];
+        const double D = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        const double e = exp(-D);
+        const double K = sf2 * ((1.0 + D) * e);
+        const double w = a == b ? 1.0 : 2.0;
+        for (int d = 0; d < 3; ++d) {
+          const double tt = cq[d * 128 + m] - cq[d * 128 + 64 + nn];
+          v[d] += w * (Q * (sf2 * ((tt * tt) * e)));
+        }
+        v[3] += w * (Q * (2.0 * K));
+        if (a == b) v[4] += Q;
+      }
+  block_sum<5>(v, red);
+  if (t == 0)
+    for (int q = 0; q < 5; ++q) part[(size_t)tile * 5 + q] = v[q];
+}
+
 // ------------------------------------------------------------------- host --
 
 struct HipErr {
@@ -274,7 +353,7 @@ struct HipErr {
     if (s_ != rocblas_status_success)                                                         \
       throw HipErr{std::string(#expr) + ": " + rocblas_status_to_string(s_)};                 \
   } while (0)
-#define KC() HC(hipGetLastError())
+#define KCHK() HC(hipGetLastError())
 
 struct Handle {
   rocblas_handle h = nullptr;
@@ -412,10 +491,17 @@ struct Buf {
   }
 };
 
+// objective pass: fused MFMA kernel (default) or, with OI_NYS_FUSED=0, the
+// rocBLAS GEMM forming Ki followed by k_nys_grad
+inline bool fused_objective() {
+  const char* e = getenv("OI_NYS_FUSED");
+  return !(e && atoi(e) == 0);
+}
+
 struct Lane {
   hipStream_t st = nullptr;
   Handle H;
-  Buf Knm, U1, ut, W, Ki, Av, tv, ks, kv, xsc, part;
+  Buf Knm, U1, ut, W, Ki, Wp, Av, tv, ks, kv, xsc, part;
   Stager sg;
   hipEvent_t done = nullptr;
   Lane(int64_t nmax, int64_t mmax, bool obj, bool pred, bool profile) {
@@ -430,7 +516,11 @@ struct Lane {
     Av.alloc(nmax * 8);
     tv.alloc(mmax * 8);
     if (obj) {
-      Ki.alloc(nmax * nmax * 8);
+      if (fused_objective()) {
+        Wp.alloc((size_t)blocks(mmax, 64) * nt * 4096 * 8);
+      } else {
+        Ki.alloc(nmax * nmax * 8);
+      }
       part.alloc(nt * nt * 5 * 8);
     }
     if (pred) {
@@ -676,7 +766,7 @@ class Runner {
         hipLaunchKernelGGL(k_nys_logdet, dim3(cnt), dim3(256), 0, st_, B0, M, M, mm,
                            stl_.as<double>() + s0 * mpmax_, mpmax_,
                            res_.as<double>() + g0 * NRES, (int64_t)NRES);
-        KC();
+        KCHK();
         BC(rocsolver_dtrtri_strided_batched(H_.h, rocblas_fill_lower, rocblas_diagonal_non_unit, iM,
                                             B0, iM, mm, tmp + cnt, cnt));
         sg_.end();
@@ -732,16 +822,16 @@ class Runner {
     L.sg.begin(S_BUILD, 0.0, 8.0 * R.dM * R.dM);
     hipLaunchKernelGGL(k_nys_scale, dim3(blocks(R.n, 256)), dim3(256), 0, st, R.x, R.n, R.hp[0],
                        R.hp[1], R.hp[2], R.sc, obj_ ? R.sq : nullptr);
-    KC();
+    KCHK();
     hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.M, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
                        R.sl, R.M, R.sc, R.sl, R.hp[3], R.Kmm, R.Mp);
-    KC();
+    KCHK();
     if (R.Mp > R.M) {
       // pad eigenvalue above every eigenvalue of K_mm (<= trace = M sf2), so the
       // M real eigenpairs stay first in syevd's ascending order
       hipLaunchKernelGGL(k_nys_pad, dim3(blocks(R.Mp, 256), (unsigned)R.Mp), dim3(256), 0, st,
                          R.Kmm, R.M, R.Mp, 2.0 * R.dM * R.hp[3] + 1.0);
-      KC();
+      KCHK();
     }
     L.sg.end();
   }
@@ -759,24 +849,24 @@ class Runner {
     L.sg.begin(S_PANEL, 4 * R.dn * R.dM * R.dM, 8.0 * R.dn * R.dM);
     hipLaunchKernelGGL(k_nys_eigpost, dim3(blocks(R.Mp, 256)), dim3(256), 0, st, R.s, R.M, R.Mp,
                        R.n, R.stl);
-    KC();
+    KCHK();
     hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
                        nullptr, R.n, R.sc, R.sl, R.hp[3], Knm, R.n);
-    KC();
+    KCHK();
     BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, R.in, R.iM, R.iM, &one, Knm,
                      R.in, R.Kmm, R.iMp, &zero, U1, R.in));
     hipLaunchKernelGGL(k_nys_ut, dim3(blocks(R.n * R.M, 256)), dim3(256), 0, st, U1, R.n, R.M, R.s,
                        std::sqrt(R.dM / R.dn), 1.0 / R.hp[4], ut, R.C);
-    KC();
+    KCHK();
     BC(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, R.iM, R.iM, R.in, &one,
                      ut, R.in, R.C, R.in, &zero, R.B, R.iMp));
     hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.B, R.M, R.Mp, R.stl, 1,
                        0.0);
-    KC();
+    KCHK();
     if (R.Mp > R.M) {
       hipLaunchKernelGGL(k_nys_pad, dim3(blocks(R.Mp, 256), (unsigned)R.Mp), dim3(256), 0, st, R.B,
                          R.M, R.Mp, 1.0);
-      KC();
+      KCHK();
     }
     L.sg.end();
   }
@@ -796,11 +886,11 @@ class Runner {
     sg.begin(S_APPLY, 2.0 * dM * dM * dn + 4.0 * dn * dM, 16.0 * dn * dM);
     hipLaunchKernelGGL(k_nys_zero_upper, dim3(blocks(R.M, 256), (unsigned)R.M), dim3(256), 0, st,
                        R.B, R.M, R.Mp);
-    KC();
+    KCHK();
     BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.iM, R.iM, &one,
                      R.C, R.in, R.B, R.iMp, &zero, Wt, R.in));
     hipLaunchKernelGGL(k_nys_vi, dim3(blocks(R.n, 256)), dim3(256), 0, st, R.r, R.n, isn2, Av);
-    KC();
+    KCHK();
     BC(rocblas_dgemv(h, rocblas_operation_transpose, R.in, R.iM, &one, Wt, R.in, R.r, 1, &zero, tv,
                      1));
     BC(rocblas_dgemv(h, rocblas_operation_none, R.in, R.iM, &mone, Wt, R.in, tv, 1, &one, Av, 1));
@@ -809,27 +899,47 @@ class Runner {
       double* Ki = L.Ki.as<double>();
       sg.begin(S_LOGDET, 2.0 * dn, 16.0 * dn);
       hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, R.r, Av, R.n, R.rs + 0);
-      KC();
+      KCHK();
       sg.end();
-      // Ki = Vi - W'W (full GEMM: rocBLAS dsyrk at this shape is ~2x slower than
-      // dgemm although it does half the flops; the sweep below reads the lower half)
-      sg.begin(S_KI, 2.0 * dn * dn * dM, 8.0 * dn * dn);
-      BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.in, R.iM,
-                       &mone, Wt, R.in, Wt, R.in, &zero, Ki, R.in));
-      hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.n, 256)), dim3(256), 0, st, Ki, R.n, R.n, nullptr,
-                         0, isn2);
-      KC();
-      sg.end();
-      // the lower triangle of Ki read once (~4 n^2 bytes); inputs and A cache-resident
-      sg.begin(S_GRAD, 0.0, 4.0 * dn * dn);
-      const unsigned nt = blocks(R.n, 64);
-      hipLaunchKernelGGL(k_nys_grad, dim3(nt, nt), dim3(256), 0, st, Ki, Av, R.sc, R.sq, R.n, sf2,
-                         L.part.as<double>());
-      KC();
-      hipLaunchKernelGGL(k_nys_partsum, dim3(1), dim3(256), 0, st, L.part.as<double>(),
-                         (int64_t)nt * nt, R.rs + 2);
-      KC();
-      sg.end();
+      if (fused_objective()) {
+        // (W'W) tiles on the MFMA core, reduced against K, dK in the same kernel
+        const int Tn = (int)blocks(R.n, 64), Tk = (int)blocks(R.M, 64);
+        const int ntri = Tn * (Tn + 1) / 2;
+        sg.begin(S_KI, dn * dn * dM, 8.0 * dn * dM);
+        hipLaunchKernelGGL(k_nys_pack, dim3((unsigned)(Tn * Tk)), dim3(256), 0, st, Wt, R.n, R.M,
+                           Tn, L.Wp.as<double>());
+        KCHK();
+        sg.end();
+        sg.begin(S_GRAD, dn * dn * dM, 0.0);
+        hipLaunchKernelGGL(k_nys_grad_mfma, dim3((unsigned)ntri), dim3(256), 0, st,
+                           L.Wp.as<double>(), Tn, Tk, Av, R.sc, R.sq, R.n, sf2, isn2,
+                           L.part.as<double>());
+        KCHK();
+        hipLaunchKernelGGL(k_nys_partsum, dim3(1), dim3(256), 0, st, L.part.as<double>(),
+                           (int64_t)ntri, R.rs + 2);
+        KCHK();
+        sg.end();
+      } else {
+        // Ki = Vi - W'W (full GEMM: rocBLAS dsyrk at this shape is ~2x slower than
+        // dgemm although it does half the flops; the sweep below reads the lower half)
+        sg.begin(S_KI, 2.0 * dn * dn * dM, 8.0 * dn * dn);
+        BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.in, R.iM,
+                         &mone, Wt, R.in, Wt, R.in, &zero, Ki, R.in));
+        hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.n, 256)), dim3(256), 0, st, Ki, R.n, R.n, nullptr,
+                           0, isn2);
+        KCHK();
+        sg.end();
+        // the lower triangle of Ki read once (~4 n^2 bytes); inputs and A cache-resident
+        sg.begin(S_GRAD, 0.0, 4.0 * dn * dn);
+        const unsigned nt = blocks(R.n, 64);
+        hipLaunchKernelGGL(k_nys_grad, dim3(nt, nt), dim3(256), 0, st, Ki, Av, R.sc, R.sq, R.n, sf2,
+                           L.part.as<double>());
+        KCHK();
+        hipLaunchKernelGGL(k_nys_partsum, dim3(1), dim3(256), 0, st, L.part.as<double>(),
+                           (int64_t)nt * nt, R.rs + 2);
+        KCHK();
+        sg.end();
+      }
     }
     if (pred_) {
       // k* = SGPkernel(x, xs=xs); fs = mean + k*.A; k*'Ki k* = |k*|^2/sn2 - |W k*|^2
@@ -838,18 +948,18 @@ class Runner {
       double* kv = L.kv.as<double>();
       hipLaunchKernelGGL(k_nys_scale, dim3(1), dim3(64), 0, st, dxs_.as<double>() + R.c * 3,
                          (int64_t)1, R.hp[0], R.hp[1], R.hp[2], L.xsc.as<double>(), nullptr);
-      KC();
+      KCHK();
       hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), 1), dim3(256), 0, st, R.sc, nullptr,
                          R.n, L.xsc.as<double>(), nullptr, sf2, ks, R.n);
-      KC();
+      KCHK();
       hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, ks, Av, R.n, R.rs + 7);
-      KC();
+      KCHK();
       hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, ks, ks, R.n, R.rs + 8);
-      KC();
+      KCHK();
       BC(rocblas_dgemv(h, rocblas_operation_transpose, R.in, R.iM, &one, Wt, R.in, ks, 1, &zero, kv,
                        1));
       hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, kv, kv, R.M, R.rs + 9);
-      KC();
+      KCHK();
       sg.end();
     }
   }
