@@ -412,8 +412,22 @@ def main_svgp(args, torch, dist, world, rank, gpu, cdev):
 
 
 # ----------------------------------------------------------------- main
+def heartbeat(period=60.0):
+    """One stderr line a minute while a long step runs (a whole-day step is
+    ~3 min inside one library call; batch runners take silence for a hang)."""
+    import threading
+    t0 = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"[bench] running {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     args = parse()
+    heartbeat()
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))

@@ -106,6 +106,23 @@ __device__ __forceinline__ bool xcd_cell_slot(int gx, int ncell, int& cell, int&
   return cell < ncell;
 }
 
+// Same cell -> XCD dealing, but the slot-0 workgroups of every cell are
+// dispatched first: in k_chol_panel slot 0 also runs the look-ahead of the
+// next diagonal tile (j + 1 serial products), the launch's longest chain, so
+// all of them start at once instead of trailing the short two-product rows.
+__device__ __forceinline__ bool xcd_cell_slot_lead0(int gx, int ncell, int& cell, int& x) {
+  const int b = blockIdx.x, t = b >> 3, g0 = (ncell + 7) >> 3;
+  if (t < g0) {
+    cell = (b & 7) + 8 * t;
+    x = 0;
+  } else {
+    const int u = t - g0;
+    cell = (b & 7) + 8 * (u / (gx - 1));
+    x = 1 + u % (gx - 1);
+  }
+  return cell < ncell;
+}
+
 // ------------------------------------------------------------- k_build
 // K + sn2*I for tile (i, j), GPR:93-94 and GPR:126; identity on padding.
 __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
@@ -380,7 +397,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
                                                    int kbeg, int gx, int ncell) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
   int ci, x;
-  if (!xcd_cell_slot(gx, ncell, ci, x)) return;
+  if (!xcd_cell_slot_lead0(gx, ncell, ci, x)) return;
   const OiCell& c = cells[list[ci]];
   const int T = c.T;
   if (j >= T || *c.status != OI_OK) return;
