@@ -50,10 +50,21 @@ __device__ __forceinline__ int acc_col(int nb) {
 // pair(p, a, b0, b1): the p-th operand triple (A tile, B tile of the left
 // half, B tile of the right half).  Register staging is a two-deep ring
 // (chunks ch+1 and ch+2 in flight while ch is multiplied out of LDS), two LDS
-// buffers; threads 0..255 stage A and B0, threads 256..511 stage B1.
+// buffers; every thread stages one 16 B piece of each of A, B0 and B1, so the
+// loads are branch-free and s_waitcnt can count them exactly.
 typedef double dv2 __attribute__((ext_vector_type(2)));
+// Operand tiles are read through global-address-space pointers: the tile
+// addresses come out of OiCell records, so the compiler would otherwise emit
+// FLAT loads, which count against lgkmcnt too -- every s_waitcnt lgkmcnt(0)
+// of the LDS reads in compute() would then also wait for the prefetch of the
+// next chunks, exposing HBM latency once per chunk.
+typedef __attribute__((address_space(1))) const dv2 gdv2;
+__device__ __forceinline__ dv2 gload2(const double* p) { return *(gdv2*)p; }
 struct StageRegs {
   dv2 a0, a1, b0, b1;
+};
+struct StageRegs3 {
+  dv2 a, b0, b1;
 };
 
 template <class PairFn>
@@ -62,31 +73,23 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
   const int wr = (w >> 2) & 1, wc = w & 3;
   const int nch = npairs * (GNB / KC);  // even
   if (nch == 0) return;
-  const int tt = t & 255, half = t >> 8;
-  const int sk = tt >> 4, sm = (tt & 15) * 4;
+  const int sk = t >> 5, sm = (t & 31) * 2;  // this thread's 16 B of a 16 x 64 chunk
   const int fr = lane & 15, fk = lane >> 4;
-  StageRegs r0, r1;
-  auto load = [&](int ch, StageRegs& q) __attribute__((always_inline)) {
+  StageRegs3 r0, r1;
+  auto load = [&](int ch, StageRegs3& q) __attribute__((always_inline)) {
     const double *pa, *pb0, *pb1;
-    pair(ch >> 2, pa, pb0, pb1);
-    const int off = (ch & 3) * KC * GNB + tt * 4;
-    if (half == 0) {
-      q.a0 = *(const dv2*)(pa + off);
-      q.a1 = *(const dv2*)(pa + off + 2);
-    }
-    const double* pb = half ? pb1 : pb0;
-    q.b0 = *(const dv2*)(pb + off);
-    q.b1 = *(const dv2*)(pb + off + 2);
+    [[clang::always_inline]] pair(ch >> 2, pa, pb0, pb1);
+    const int off = (ch & 3) * KC * GNB + t * 2;
+    q.a = gload2(pa + off);
+    q.b0 = gload2(pb0 + off);
+    q.b1 = gload2(pb1 + off);
   };
-  auto store = [&](int buf, const StageRegs& q) __attribute__((always_inline)) {
+  auto store = [&](int buf, const StageRegs3& q) __attribute__((always_inline)) {
     double* As = lds + buf * (STAGE_A + STAGE_B);
     double* Bs = As + STAGE_A;
-    if (half == 0) {
-      *(dv2*)(As + sk * LDSA + sm) = q.a0;
-      *(dv2*)(As + sk * LDSA + sm + 2) = q.a1;
-    }
-    *(dv2*)(Bs + sk * LDSB + 64 * half + sm) = q.b0;
-    *(dv2*)(Bs + sk * LDSB + 64 * half + sm + 2) = q.b1;
+    *(dv2*)(As + sk * LDSA + sm) = q.a;
+    *(dv2*)(Bs + sk * LDSB + sm) = q.b0;
+    *(dv2*)(Bs + sk * LDSB + 64 + sm) = q.b1;
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
     const double* As = lds + buf * (STAGE_A + STAGE_B);
@@ -108,12 +111,15 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
   load(1, r1);
   store(0, r0);
   __syncthreads();
+  // The prefetches are unconditional (the last ones re-read the final chunk,
+  // unused): a conditional load makes s_waitcnt merge "issued" and "skipped"
+  // paths and wait for the newest loads too, serialising the ring.
   for (int ch = 0; ch < nch; ch += 2) {
-    if (ch + 2 < nch) load(ch + 2, r0);
+    load(min(ch + 2, nch - 1), r0);
     compute(0);
     store(1, r1);
     __syncthreads();
-    if (ch + 3 < nch) load(ch + 3, r1);
+    load(min(ch + 3, nch - 1), r1);
     compute(1);
     if (ch + 2 < nch) store(0, r0);
     __syncthreads();
@@ -148,12 +154,12 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs,
   StageRegs r0, r1;
   auto load = [&](int ch, StageRegs& q) __attribute__((always_inline)) {
     const double *pa, *pb;
-    pair(ch >> 2, pa, pb);
+    [[clang::always_inline]] pair(ch >> 2, pa, pb);
     const int off = (ch & 3) * KC * GNB + t * 4;
-    q.a0 = *(const dv2*)(pa + off);
-    q.a1 = *(const dv2*)(pa + off + 2);
-    q.b0 = *(const dv2*)(pb + off);
-    q.b1 = *(const dv2*)(pb + off + 2);
+    q.a0 = gload2(pa + off);
+    q.a1 = gload2(pa + off + 2);
+    q.b0 = gload2(pb + off);
+    q.b1 = gload2(pb + off + 2);
   };
   auto store = [&](int buf, const StageRegs& q) __attribute__((always_inline)) {
     double* As = lds + buf * 2 * STAGE_A;
@@ -183,12 +189,13 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs,
   load(1, r1);
   store(0, r0);
   __syncthreads();
+  // unconditional prefetches: see gemm2_kmajor
   for (int ch = 0; ch < nch; ch += 2) {
-    if (ch + 2 < nch) load(ch + 2, r0);
+    load(min(ch + 2, nch - 1), r0);
     compute(0);
     store(1, r1);
     __syncthreads();
-    if (ch + 3 < nch) load(ch + 3, r1);
+    load(min(ch + 3, nch - 1), r1);
     compute(1);
     if (ch + 2 < nch) store(0, r0);
     __syncthreads();

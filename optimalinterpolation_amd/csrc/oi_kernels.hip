@@ -34,7 +34,7 @@
 #include "oi_gemm.h"
 
 // GEMM1(acc, lds, npairs, pair): the 64x64 tile-GEMM loop of the panel / lauum kernels
-#define GEMM1(acc, lds, np, fn) gemm1_kmajor(acc, lds, np, fn)
+#define GEMM1(acc, lds, np, ...) gemm1_kmajor(acc, lds, np, __VA_ARGS__)
 
 #define NB OI_NB
 #define SQRT3 1.7320508075688772
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   quad_zero(acc);
   if (x < ntrsm) {
     const int i = j + 1 + x;
-    GEMM1(acc, lds, j + 1 - kbeg, [&](int p, const double*& a, const double*& b) {
+    GEMM1(acc, lds, j + 1 - kbeg, [=, &c](int p, const double*& a, const double*& b) {
       const int k = kbeg + p;
       a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
       b = tileL(c, i, k);  // k == j: A_ij, already holding A_ij - sum_{k<kbeg} L_ik L_jk^T
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       }
     }
     __syncthreads();
-    GEMM1(accd, lds, j, [&](int p, const double*& a, const double*& b) {
+    GEMM1(accd, lds, j, [=, &c](int p, const double*& a, const double*& b) {
       a = tileL(c, i, p);
       b = a;
     });
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   // kbeg > jj: W_j,jj holds Vneg = -sum_{k=jj}^{kbeg-1} L_jk W_k,jj (k_panel_even), so
   // W_j,jj = sum_{k=kbeg}^{j-1} P_jk W_k,jj + Dinv_jj Vneg
   const int kfirst = jj > kbeg ? jj : kbeg, extra = kbeg > jj ? 1 : 0;
-  GEMM1(acc, lds, j - kfirst + extra, [&](int p, const double*& a, const double*& b) {
+  GEMM1(acc, lds, j - kfirst + extra, [=, &c](int p, const double*& a, const double*& b) {
     const int k = kfirst + p;
     a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
     b = tileW(c, k, jj);  // k == j: Vneg
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   if (x < ntrsm) {
     const int i = j + 1 + x;
     gemm2_kmajor(acc, lds, j + 1,
-                 [&](int p, const double*& a, const double*& b0, const double*& b1) {
+                 [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
                    if (p < j) {
                      a = tileL(c, i, p);
                      b0 = Pj + (size_t)p * OI_TILE;
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   }
   const int jj = x - ntrsm;
   if (c.mode != OI_MODE_EVAL || jj >= j) return;
-  gemm2_kmajor(acc, lds, j - jj, [&](int p, const double*& a, const double*& b0, const double*& b1) {
+  gemm2_kmajor(acc, lds, j - jj, [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
     const int k = jj + p;
     a = tileW(c, k, jj);
     b0 = Pj + (size_t)k * OI_TILE;
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
   if (*c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
   Quad acc;
   quad_zero(acc);
-  GEMM1(acc, lds, T - i, [&](int p, const double*& a, const double*& b) {
+  GEMM1(acc, lds, T - i, [=, &c](int p, const double*& a, const double*& b) {
     a = tileW(c, i + p, i);
     b = tileW(c, i + p, j);
   });
