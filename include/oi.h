@@ -75,6 +75,40 @@ int oi_gpr_batch(const double* xyt, const double* z, const int64_t* offs, int64_
                  const double* hyp, double* out, int32_t* status, int32_t* info,
                  const oi_options* opts);
 
+/* Stream ordering (opts->device_inputs = 1): device inputs are read on
+ * opts->stream when it is set; with stream == NULL the library's own stream
+ * first waits for the legacy NULL stream (PyTorch's default stream), so any
+ * producer of xyt / z / y / mX queued there has finished.  A producer on
+ * another stream must pass that stream.  Host outputs are complete on return. */
+
+/* ---- session: continuous batching across calls ------------------------
+ * The per-cell loops GPR:258-261 / GPR:316-319 as a stream of batches: every
+ * submitted batch (same arguments and semantics as oi_gpr_batch) joins one
+ * queue; cells are admitted largest-n first within a batch and FIFO across
+ * batches, so cells of the next batch fill the GPU while the previous one's
+ * slowest cells finish.  Per-cell results are bitwise the same as one
+ * oi_gpr_batch call's (they never depend on which cells share a round).
+ *   oi_session_submit  returns a ticket >= 0 (or a negative OI_E* code).  Host
+ *                      metadata (offs, xs, x0, hyp) and host inputs are copied
+ *                      before it returns; DEVICE inputs and all outputs must
+ *                      stay valid until the ticket completes.
+ *   oi_session_wait    runs rounds until the ticket completes (ticket < 0: all
+ *                      submitted work); it may return with later batches'
+ *                      rounds still in flight on the device.
+ *   oi_session_done    1 if the ticket has completed, else 0.
+ *   oi_session_destroy waits for in-flight rounds and frees the session
+ *                      (unfinished cells are dropped, outputs left unwritten).
+ * A session is used from one thread at a time. */
+typedef struct oi_session oi_session;
+oi_session* oi_session_create(const oi_options* opts);
+int64_t oi_session_submit(oi_session* s, const double* xyt, const double* z, const int64_t* offs,
+                          int64_t ncell, const double* xs, double mean, const double* x0,
+                          int32_t opt, const double* hyp, double* out, int32_t* status,
+                          int32_t* info);
+int oi_session_wait(oi_session* s, int64_t ticket);
+int oi_session_done(oi_session* s, int64_t ticket);
+void oi_session_destroy(oi_session* s);
+
 /* SMLII (GPR:107-141) for a batch of cells at fixed log-hypers.
  *   xyt, offs as above; y [N] outputs; mX [N] prior mean per observation
  *   h   [ncell x 6] log-hypers (lx, ly, lt, sf2, sn2, unused)

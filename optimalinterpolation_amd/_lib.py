@@ -35,7 +35,8 @@ EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_cr
            'oi_cg_step', 'oi_cg_feed', 'oi_cg_result', 'oi_cg_destroy', 'oi_last_error',
            'oi_version', 'oi_profile_json', 'oi_profile_reset', 'oi_smooth_fields',
            'oi_ball_query', 'oi_gather_rows', 'oi_nystrom_batch',
-           'oi_nystrom_fit_batch', 'oi_svgp_batch', 'oi_svgp_param_count')
+           'oi_nystrom_fit_batch', 'oi_svgp_batch', 'oi_svgp_param_count', 'oi_session_create',
+           'oi_session_submit', 'oi_session_wait', 'oi_session_done', 'oi_session_destroy')
 
 
 class OiOptions(ctypes.Structure):
@@ -117,6 +118,18 @@ def load():
                                       c_double_p, c_double_p, c_double_p, c_int32_p,
                                       ctypes.POINTER(OiOptions)]
         lib.oi_svgp_batch.restype = ctypes.c_int
+        lib.oi_session_create.argtypes = [ctypes.POINTER(OiOptions)]
+        lib.oi_session_create.restype = ctypes.c_void_p
+        lib.oi_session_submit.argtypes = [ctypes.c_void_p, c_double_p, c_double_p, c_int64_p,
+                                          ctypes.c_int64, c_double_p, ctypes.c_double, c_double_p,
+                                          ctypes.c_int32, c_double_p, c_double_p, c_int32_p, c_int32_p]
+        lib.oi_session_submit.restype = ctypes.c_int64
+        lib.oi_session_wait.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        lib.oi_session_wait.restype = ctypes.c_int
+        lib.oi_session_done.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        lib.oi_session_done.restype = ctypes.c_int
+        lib.oi_session_destroy.argtypes = [ctypes.c_void_p]
+        lib.oi_session_destroy.restype = None
         _lib = lib
         return lib
 
@@ -174,25 +187,56 @@ def gpr_batch(xyt, z, offs, xs, mean, x0=None, opt=True, hyp=None, info=False, *
     return out, status, inf
 
 
+def _check_dev(t, device, dtype='float64', n=None, what='tensor'):
+    """A device tensor handed to liboi: right dtype, on cuda:<device>,
+    contiguous, ``n`` elements (liboi reads 8 bytes per element)."""
+    if str(t.dtype) != f'torch.{dtype}':
+        raise ValueError(f"{what} must be torch.{dtype}, got {t.dtype}")
+    if t.device.type != 'cuda' or (t.device.index if t.device.index is not None else 0) != int(device):
+        raise ValueError(f"{what} must live on cuda:{device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what} must be contiguous")
+    if n is not None and t.numel() != n:
+        raise ValueError(f"{what} has {t.numel()} elements, expected {n}")
+
+
+def _sync_producers(device):
+    """The Nystrom / SVGP entry points run on private non-blocking streams:
+    wait here until torch's current stream has produced their device inputs."""
+    import torch
+    torch.cuda.current_stream(int(device)).synchronize()
+
+
+def _caller_stream(device):
+    """torch's current stream on ``device`` as a hipStream_t (None = the
+    legacy NULL stream, which the library then waits for itself)."""
+    import torch
+    h = torch.cuda.current_stream(device).cuda_stream
+    return h or None
+
+
 def gpr_batch_device(xyt_dev, z_dev, offs, xs, mean, x0=None, opt=True, hyp=None, info=False,
                      **opt_kw):
     """oi_gpr_batch with inputs already resident in HBM: ``xyt_dev`` / ``z_dev``
-    are device tensors (anything with ``data_ptr()``, fp64, contiguous) on
-    ``opt_kw['device']``; the metadata stays on the host."""
+    are fp64 contiguous torch tensors on cuda:``opt_kw['device']``; the
+    metadata stays on the host.  Launches are ordered after torch's current
+    stream (include/oi.h, stream ordering)."""
     lib = load()
     offs = np.ascontiguousarray(offs, dtype=np.int64)
     xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1, 3)
     ncell = len(offs) - 1
     N = int(offs[-1])
-    if xs.shape[0] != ncell or offs[0] != 0 or z_dev.numel() != N or xyt_dev.numel() != 3 * N:
+    dev = int(opt_kw.get('device', 0))
+    if xs.shape[0] != ncell or offs[0] != 0:
         raise ValueError("inconsistent ragged batch")
-    if not (xyt_dev.is_contiguous() and z_dev.is_contiguous()):
-        raise ValueError("device inputs must be contiguous")
+    _check_dev(xyt_dev, dev, n=3 * N, what='xyt')
+    _check_dev(z_dev, dev, n=N, what='z')
     out = np.empty((ncell, 8))
     status = np.zeros(ncell, dtype=np.int32)
     inf = np.zeros((ncell, 4), dtype=np.int32) if info else None
     x0a = np.ascontiguousarray(x0, dtype=np.float64) if x0 is not None else None
     hypa = np.ascontiguousarray(hyp, dtype=np.float64).reshape(-1, 5) if hyp is not None else None
+    opt_kw.setdefault('stream', _caller_stream(dev))
     o = options(device_inputs=True, **opt_kw)
     rc = lib.oi_gpr_batch(ctypes.cast(xyt_dev.data_ptr(), c_double_p),
                           ctypes.cast(z_dev.data_ptr(), c_double_p),
@@ -202,6 +246,94 @@ def gpr_batch_device(xyt_dev, z_dev, offs, xs, mean, x0=None, opt=True, hyp=None
                           _ptr(status, ctypes.c_int32), _ptr(inf, ctypes.c_int32), ctypes.byref(o))
     _check(rc)
     return out, status, inf
+
+
+class Session:
+    """oi_session_*: continuous batching across calls (include/oi.h).
+
+    ``submit`` takes the oi_gpr_batch arguments (host numpy arrays, or fp64
+    device tensors with ``device_inputs=True``) and returns a ticket;
+    ``wait(ticket)`` returns that batch's (out, status, info) once complete,
+    leaving later batches' rounds running on the GPU.  Cells of consecutive
+    batches share rounds, so a stream of small batches runs at the rate of one
+    big call; per-cell results equal oi_gpr_batch's bit for bit."""
+
+    def __init__(self, device=0, device_inputs=False, **opt_kw):
+        self._lib = load()
+        self.device = int(device)
+        self.device_inputs = bool(device_inputs)
+        if self.device_inputs:
+            opt_kw.setdefault('stream', _caller_stream(self.device))
+        self._opts = options(device=device, device_inputs=device_inputs, **opt_kw)
+        self._h = self._lib.oi_session_create(ctypes.byref(self._opts))
+        if not self._h:
+            raise OiError(f"oi_session_create: {self._lib.oi_last_error().decode(errors='replace')}")
+        self._live = {}
+
+    def submit(self, xyt, z, offs, xs, mean, x0=None, opt=True, hyp=None):
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1, 3)
+        ncell = len(offs) - 1
+        N = int(offs[-1]) if ncell >= 0 else 0
+        if xs.shape[0] != ncell or offs[0] != 0:
+            raise ValueError("inconsistent ragged batch")
+        if self.device_inputs:
+            _check_dev(xyt, self.device, n=3 * N, what='xyt')
+            _check_dev(z, self.device, n=N, what='z')
+            px, pz = _dptr(xyt), _dptr(z)
+        else:
+            xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+            z = np.ascontiguousarray(z, dtype=np.float64)
+            if xyt.shape[0] != N or len(z) != N:
+                raise ValueError("inconsistent ragged batch")
+            px, pz = _ptr(xyt, ctypes.c_double), _ptr(z, ctypes.c_double)
+        x0a = np.ascontiguousarray(x0, dtype=np.float64) if x0 is not None else None
+        hypa = np.ascontiguousarray(hyp, dtype=np.float64).reshape(-1, 5) if hyp is not None else None
+        if opt and (x0a is None or x0a.shape != (6,)):
+            raise ValueError("opt=True needs x0 of length 6")
+        if not opt and (hypa is None or hypa.shape[0] != ncell):
+            raise ValueError("opt=False needs hyp [ncell x 5]")
+        out = np.empty((ncell, 8))
+        status = np.zeros(ncell, dtype=np.int32)
+        info = np.zeros((ncell, 4), dtype=np.int32)
+        t = self._lib.oi_session_submit(self._h, px, pz, _ptr(offs, ctypes.c_int64), ncell,
+                                        _ptr(xs, ctypes.c_double), float(mean),
+                                        _ptr(x0a, ctypes.c_double), 1 if opt else 0,
+                                        _ptr(hypa, ctypes.c_double), _ptr(out, ctypes.c_double),
+                                        _ptr(status, ctypes.c_int32), _ptr(info, ctypes.c_int32))
+        if t < 0:
+            _check(int(t))
+        # device inputs and the outputs must outlive the ticket
+        self._live[int(t)] = (out, status, info, xyt, z)
+        return int(t)
+
+    def done(self, ticket):
+        return self._lib.oi_session_done(self._h, int(ticket)) == 1
+
+    def wait(self, ticket=-1):
+        """Block until ``ticket`` completes (all work when -1); returns its
+        (out, status, info), or None for ticket -1."""
+        _check(self._lib.oi_session_wait(self._h, int(ticket)))
+        if ticket < 0:
+            self._live.clear()
+            return None
+        out, status, info, _, _ = self._live.pop(int(ticket))
+        return out, status, info
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._lib.oi_session_destroy(self._h)
+            self._h = None
+            self._live.clear()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        self.close()
 
 
 def nlml_grad_batch(xyt, y, mX, offs, h, **opt_kw):
@@ -278,6 +410,7 @@ def nystrom_fit_batch(xyt, y, offs, sel, soffs, x0, xs, mean, **opt_kw):
         if xyt.numel() != 3 * offs[-1] or y.numel() != offs[-1]:
             raise ValueError("inconsistent ragged batch")
         px, py = _dptr(xyt), _dptr(y)
+        _sync_producers(opt_kw.get('device', 0))
     else:
         xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
         y = np.ascontiguousarray(y, dtype=np.float64)
@@ -312,7 +445,10 @@ def svgp_batch(xyt, y, offs, Z0, init, xs, batch=100, iterations=10000, log_ever
     init = np.ascontiguousarray(init, dtype=np.float64).reshape(ncell, 6)
     xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(ncell, 3)
     if opt_kw.get('device_inputs'):
+        if xyt.numel() != 3 * offs[-1] or y.numel() != offs[-1]:
+            raise ValueError("inconsistent ragged batch")
         px, py = _dptr(xyt), _dptr(y)
+        _sync_producers(opt_kw.get('device', 0))
     else:
         xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
         y = np.ascontiguousarray(y, dtype=np.float64)
@@ -378,7 +514,14 @@ class CG:
 
 
 def _dptr(t, ctype=ctypes.c_double):
-    """Device pointer of a torch tensor (plumbing for device_inputs=1 calls)."""
+    """Device pointer of a torch tensor (plumbing for device_inputs=1 calls),
+    after checking what liboi assumes: a contiguous CUDA tensor whose element
+    type matches ``ctype`` (fp64 or int64, 8 bytes per element)."""
+    want = {ctypes.c_double: 'torch.float64', ctypes.c_int64: 'torch.int64'}[ctype]
+    if str(t.dtype) != want:
+        raise ValueError(f"device array must be {want}, got {t.dtype}")
+    if t.device.type != 'cuda':
+        raise ValueError(f"device array must be a CUDA tensor, got {t.device}")
     if not t.is_contiguous():
         raise ValueError("device arrays must be contiguous")
     return ctypes.cast(t.data_ptr(), ctypes.POINTER(ctype))

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -178,6 +179,7 @@ struct Context {
   }
   Arena arena;
   size_t arena_bytes = 0;
+  int live_sessions = 0;  // the arena is never re-sized under a live session
   std::mutex mu;
 };
 
@@ -196,16 +198,29 @@ Context& context(int device, int64_t pool_bytes) {
   HIPC(hipSetDevice(device));
   size_t want = (size_t)pool_bytes;
   if (want == 0) {
-    if (p->arena_bytes) return *p;  // keep the automatic arena between calls
+    if (p->arena_bytes == SIZE_MAX - 1) return *p;  // keep the automatic arena between calls
     size_t fr = 0, tot = 0;
     HIPC(hipMemGetInfo(&fr, &tot));
     want = (size_t)(fr * 0.6);
   }
-  if (want != p->arena_bytes) {
+  if (want != p->arena_bytes && p->live_sessions == 0) {
     p->arena.~Arena();
     new (&p->arena) Arena();
-    p->arena.init(want);
-    p->arena_bytes = want;
+    p->arena_bytes = 0;
+    // several processes sharing a device size their arenas from the same
+    // hipMemGetInfo snapshot: on failure, halve the automatic size and retry
+    const bool automatic = pool_bytes == 0;
+    while (true) {
+      try {
+        p->arena.init(want);
+        break;
+      } catch (const HipError&) {
+        (void)hipGetLastError();
+        if (!automatic || want < (size_t(1) << 30)) throw;
+        want /= 2;
+      }
+    }
+    p->arena_bytes = automatic ? SIZE_MAX - 1 : want;  // automatic: keep between calls
   }
   return *p;
 }
@@ -241,30 +256,39 @@ struct HBuf {  // pinned host
 };
 
 // ------------------------------------------------------------- the batch
+// One submitted ragged batch of cells ("ticket").  Host metadata is copied at
+// submission; host inputs are copied to the device at submission; outputs go
+// to the caller's arrays as each cell finishes.
 struct Job {
-  // inputs (host, or device when opts.device_inputs)
-  const double* xyt;
-  const int64_t* offs;
-  int64_t ncell;
-  const double* y = nullptr;    // observations
-  const double* mX = nullptr;   // per-observation prior mean, or null => `mean`
-  const double* xs = nullptr;   // ncell x 3 (predict)
+  // inputs (device after submission)
+  const double* xyt = nullptr;  // device rows of the batch (caller's or own copy)
+  const double* r = nullptr;    // device residuals y - mX
+  std::vector<int64_t> offs;    // ncell + 1
+  int64_t ncell = 0;
+  std::vector<double> xs;       // ncell x 3 (predict)
   double mean = 0.0;
   // per-cell work description
-  enum Kind { FIT_PREDICT, PREDICT_ONLY, EVAL_ONLY } kind;
-  const double* x0 = nullptr;
-  const double* hyp = nullptr;  // PREDICT_ONLY: ncell x 5
-  const double* h = nullptr;    // EVAL_ONLY: ncell x 6
+  enum Kind { FIT_PREDICT, PREDICT_ONLY, EVAL_ONLY } kind = FIT_PREDICT;
+  std::vector<double> x0;       // FIT_PREDICT: 6
+  std::vector<double> hyp;      // PREDICT_ONLY: ncell x 5
+  std::vector<double> h;        // EVAL_ONLY: ncell x 6
   oi::CgOptions cg;
-  // outputs
+  // outputs (caller-owned)
   double* out = nullptr;        // FIT/PRED: ncell x 8
   int32_t* status = nullptr;
   int32_t* info = nullptr;
   double* nlz = nullptr;        // EVAL_ONLY
   double* grad = nullptr;
+  // bookkeeping
+  int64_t id = 0;
+  int64_t remaining = 0;
+  size_t in_off = SIZE_MAX, in_bytes = 0;  // arena block holding xyt copy + r
+  DBuf own;                                // fallback when the arena is full
+  std::vector<double> r_host;              // staging for host inputs
 };
 
 struct Slot {
+  Job* job = nullptr;
   int64_t cell = -1;
   size_t off = 0, bytes = 0;
   int phase = 0;  // 0 fit (eval), 1 predict, 2 eval-only
@@ -274,85 +298,183 @@ struct Slot {
   oi::CgResult res;
 };
 
-int run(const Job& job, const oi_options& o) {
-  auto t_start = std::chrono::steady_clock::now();
-  Context& ctx = context(o.device, o.pool_bytes);
-  std::lock_guard<std::mutex> lk(ctx.mu);
-  HIPC(hipSetDevice(ctx.device));
-  hipStream_t st = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
-  const int64_t ncell = job.ncell;
-  const int64_t N = job.offs[ncell];
-
-  // inputs to device once; residuals r = y - mX (GPR:127, GPR:178)
-  DBuf d_xyt_own, d_r, d_y_own, d_m_own;
-  const double* d_xyt = job.xyt;
-  d_r.reserve(std::max<size_t>(N * 8, 256));
-  if (!o.device_inputs) {
-    d_xyt_own.reserve(std::max<size_t>(N * 3 * 8, 256));
-    d_xyt = (const double*)d_xyt_own.p;
-    if (N > 0) {
-      std::vector<double> r(N);
-      for (int64_t a = 0; a < N; ++a) r[a] = job.y[a] - (job.mX ? job.mX[a] : 1.0 * job.mean);
-      HIPC(hipMemcpyAsync(d_xyt_own.p, job.xyt, N * 3 * 8, hipMemcpyHostToDevice, st));
-      HIPC(hipMemcpyAsync(d_r.p, r.data(), N * 8, hipMemcpyHostToDevice, st));
-      HIPC(hipStreamSynchronize(st));  // r is a local host buffer
+// Continuous-batching engine over one device context.  Cells of every
+// submitted batch wait in one FIFO queue (largest n first inside a batch) and
+// are admitted while the arena has room; rounds evaluate every resident cell.
+// wait(id) drives rounds until batch `id` is complete and returns with the
+// next round already in flight, so the GPU keeps working while the caller
+// submits more batches (oi_session_*); a one-shot oi_gpr_batch is
+// submit + drain on a private engine.
+class Engine {
+ public:
+  Engine(Context& ctx, const oi_options& o, int64_t cap_hint)
+      : ctx_(ctx), o_(o), legacy_(legacy_panels()) {
+    HIPC(hipSetDevice(ctx.device));
+    st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
+    static const bool debug_set = [] {
+      const char* e = getenv("OI_DEBUG");
+      if (e && atoi(e) == 1) oi_set_debug(1);
+      return true;
+    }();
+    (void)debug_set;
+    const char* ep = getenv("OI_POISON");
+    poison_ = ep && atoi(ep) == 1;
+    cap_ = (int)std::max<int64_t>(1, std::min<int64_t>(cap_hint, o.max_pool > 0 ? o.max_pool : 2048));
+    slots_ = std::vector<Slot>(cap_);
+    // Resident cells are split into G groups with their own stream: while one
+    // group's round runs, the host consumes the other group's results and its
+    // kernels fill the GPU around the first group's latency-bound launches.
+    G_ = 1;  // OI_GROUPS=2..8: measured no gain on the day workload (round 1)
+    if (const char* eg = getenv("OI_GROUPS")) G_ = std::max(1, std::min(8, atoi(eg)));
+    if (cap_ < 2 * G_) G_ = 1;
+    capG_ = (cap_ + G_ - 1) / G_;
+    d_cells_.reserve(cap_ * sizeof(OiCell));
+    h_cells_.reserve(cap_ * sizeof(OiCell));
+    d_list_.reserve((size_t)G_ * capG_ * 4 * 3);
+    h_list_.reserve((size_t)G_ * capG_ * 4 * 3);
+    d_res_.reserve(cap_ * OI_OUT_N * 8);
+    h_res_.reserve(cap_ * OI_OUT_N * 8);
+    d_stat_.reserve(cap_ * 4);
+    h_stat_.reserve(cap_ * 4);
+    hc_ = (OiCell*)h_cells_.p;
+    dc_ = (const OiCell*)d_cells_.p;
+    hres_ = (double*)h_res_.p;
+    hst_ = (int32_t*)h_stat_.p;
+    groups_.resize(G_);
+    for (int g = 0; g < G_; ++g) {
+      Group& gr = groups_[g];
+      gr.s0 = g * capG_;
+      gr.cap = std::max(0, std::min(capG_, cap_ - g * capG_));
+      gr.st = g == 0 ? st_ : ctx.aux_stream(g);
+      for (int s = gr.s0 + gr.cap - 1; s >= gr.s0; --s) gr.free_slots.push_back(s);
+      gr.hl = (int32_t*)h_list_.p + (size_t)g * capG_ * 3;
+      gr.dl = (int32_t*)d_list_.p + (size_t)g * capG_ * 3;
+      if (o.profile) {
+        gr.ev.resize(2 * (3 * 1024 + 16));
+        for (auto& ee : gr.ev) HIPC(hipEventCreate(&ee));
+      }
     }
-  } else if (N > 0) {
-    if (oi_launch_residual(job.y, job.mX, job.mean, (double*)d_r.p, N, st))
-      throw HipError("residual kernel launch failed");
+    HIPC(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+    t_start_ = std::chrono::steady_clock::now();
   }
-  const bool eval_mem = job.kind != Job::PREDICT_ONLY;
-  const bool legacy = legacy_panels();
-  static const bool debug_set = [] {
-    const char* e = getenv("OI_DEBUG");
-    if (e && atoi(e) == 1) oi_set_debug(1);
-    return true;
-  }();
-  (void)debug_set;
-  const bool poison = [] {
-    const char* e = getenv("OI_POISON");
-    return e && atoi(e) == 1;
-  }();
 
-  // admission order: largest cells first (cost ~ n^3), ties by index
-  std::vector<int64_t> order(ncell);
-  std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-    return job.offs[a + 1] - job.offs[a] > job.offs[b + 1] - job.offs[b];
-  });
-  size_t max_cell = 0;
-  for (int64_t c = 0; c < ncell; ++c)
-    max_cell = std::max(max_cell, cell_bytes(job.offs[c + 1] - job.offs[c], eval_mem));
-  if (max_cell > ctx.arena.size())
-    return fail(OI_E_NOMEM, "a cell needs " + std::to_string(max_cell) + " bytes of workspace, pool is " +
-                                std::to_string(ctx.arena.size()));
+  ~Engine() {
+    // never leave a round running over memory the engine is about to free
+    for (Group& gr : groups_)
+      if (gr.inflight) (void)hipStreamSynchronize(gr.st);
+    for (Group& gr : groups_)
+      for (auto& ee : gr.ev) (void)hipEventDestroy(ee);
+    if (ready_) (void)hipEventDestroy(ready_);
+    for (auto& sl : slots_)
+      if (sl.cell >= 0) ctx_.arena.release(sl.off, sl.bytes);
+    for (auto& kv : jobs_)
+      if (kv.second->in_off != SIZE_MAX) ctx_.arena.release(kv.second->in_off, kv.second->in_bytes);
+    flush_stats();
+  }
 
-  const int cap = (int)std::min<int64_t>(ncell, o.max_pool > 0 ? o.max_pool : 2048);
-  std::vector<Slot> slots(cap);
+  // Takes ownership of `job` (metadata filled by the caller; `y`, `mX`, `xyt_in`
+  // are the caller's input pointers, host or device per o.device_inputs).
+  int64_t submit(std::unique_ptr<Job> job, const double* xyt_in, const double* y, const double* mX) {
+    Job& jb = *job;
+    jb.id = next_id_++;
+    const int64_t N = jb.offs[jb.ncell];
+    size_t max_cell = 0;
+    for (int64_t c = 0; c < jb.ncell; ++c)
+      max_cell = std::max(max_cell, cell_bytes(jb.offs[c + 1] - jb.offs[c], jb.kind != Job::PREDICT_ONLY));
+    if (max_cell > ctx_.arena.size())
+      throw NoMem("a cell needs " + std::to_string(max_cell) + " bytes of workspace, pool is " +
+                  std::to_string(ctx_.arena.size()));
+    // device inputs: order after the caller's stream (or the legacy null
+    // stream, torch's default) so producers of xyt / y / mX have finished
+    if (o_.device_inputs && N > 0) {
+      HIPC(hipEventRecord(ready_, o_.stream ? (hipStream_t)o_.stream : (hipStream_t)0));
+      for (Group& gr : groups_) HIPC(hipStreamWaitEvent(gr.st, ready_, 0));
+    }
+    // workspace for the residuals (and the host inputs' device copy)
+    const size_t rb = (size_t)std::max<int64_t>(N, 1) * 8;
+    const size_t xb = o_.device_inputs ? 0 : (size_t)std::max<int64_t>(N, 1) * 24;
+    jb.in_bytes = ((rb + 255) & ~size_t(255)) + xb;
+    jb.in_off = ctx_.arena.alloc(jb.in_bytes);
+    char* base;
+    if (jb.in_off != SIZE_MAX) {
+      base = ctx_.arena.ptr(jb.in_off);
+    } else {
+      jb.own.reserve(jb.in_bytes);
+      base = (char*)jb.own.p;
+    }
+    double* d_r = (double*)base;
+    jb.r = d_r;
+    if (o_.device_inputs) {
+      jb.xyt = xyt_in;
+      if (N > 0 && oi_launch_residual(y, mX, jb.mean, d_r, N, st_))
+        throw HipError("residual kernel launch failed");
+    } else {
+      double* d_x = (double*)(base + ((rb + 255) & ~size_t(255)));
+      jb.xyt = d_x;
+      if (N > 0) {
+        jb.r_host.resize(N);
+        for (int64_t a = 0; a < N; ++a) jb.r_host[a] = y[a] - (mX ? mX[a] : 1.0 * jb.mean);
+        HIPC(hipMemcpyAsync(d_x, xyt_in, N * 3 * 8, hipMemcpyHostToDevice, st_));
+        HIPC(hipMemcpyAsync(d_r, jb.r_host.data(), N * 8, hipMemcpyHostToDevice, st_));
+        HIPC(hipStreamSynchronize(st_));  // host inputs may be released on return
+      }
+    }
+    if (G_ > 1) {  // the other groups' streams see the inputs
+      HIPC(hipEventRecord(ready_, st_));
+      for (Group& gr : groups_)
+        if (gr.st != st_) HIPC(hipStreamWaitEvent(gr.st, ready_, 0));
+    }
+    // admission order inside the batch: largest cells first (cost ~ n^3), ties by index
+    std::vector<int64_t> order(jb.ncell);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      return jb.offs[a + 1] - jb.offs[a] > jb.offs[b + 1] - jb.offs[b];
+    });
+    jb.remaining = jb.ncell;
+    Job* jp = job.get();
+    const int64_t id = jb.id;
+    for (int64_t c : order) queue_.push_back({jp, c});
+    if (jb.ncell == 0)
+      release_job(jp);
+    else
+      jobs_[id] = std::move(job);
+    return id;
+  }
 
-  // Resident cells are split into G groups with their own stream: while one
-  // group's round runs, the host consumes the other group's results and its
-  // kernels fill the GPU around the first group's latency-bound launches.
-  int G = 1;  // OI_GROUPS=2..8: measured no gain on the day workload (round 1)
-  if (const char* eg = getenv("OI_GROUPS")) G = std::max(1, std::min(8, atoi(eg)));
-  if (cap < 2 * G) G = 1;
-  const int capG = (cap + G - 1) / G;
+  bool done(int64_t id) const { return id < next_id_ && !jobs_.count(id); }
 
-  DBuf d_cells, d_list, d_res, d_stat;
-  HBuf h_cells, h_list, h_res, h_stat;
-  d_cells.reserve(cap * sizeof(OiCell));
-  h_cells.reserve(cap * sizeof(OiCell));
-  d_list.reserve((size_t)G * capG * 4 * 3);
-  h_list.reserve((size_t)G * capG * 4 * 3);
-  d_res.reserve(cap * OI_OUT_N * 8);
-  h_res.reserve(cap * OI_OUT_N * 8);
-  d_stat.reserve(cap * 4);
-  h_stat.reserve(cap * 4);
-  OiCell* hc = (OiCell*)h_cells.p;
-  const OiCell* dc = (const OiCell*)d_cells.p;
-  double* hres = (double*)h_res.p;
-  int32_t* hst = (int32_t*)h_stat.p;
+  // Drive rounds until batch `id` (or every batch, id < 0) is complete.
+  void wait(int64_t id) {
+    const auto tw = std::chrono::steady_clock::now();
+    while (true) {
+      bool any = false;
+      for (Group& gr : groups_) {
+        if (gr.inflight) consume(gr);
+        admit(gr);
+        if (!gr.active.empty()) {
+          launch_round(gr);
+          any = true;
+        }
+      }
+      if (id >= 0 ? done(id) : (jobs_.empty() && !any)) break;
+      if (!any) {
+        if (!queue_.empty()) throw NoMem("workspace exhausted with no resident cell");
+        break;
+      }
+    }
+    if (id < 0)
+      for (Group& gr : groups_)
+        if (gr.inflight) consume(gr);
+    wall_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
+    flush_stats();
+  }
 
+  struct NoMem {
+    std::string msg;
+    explicit NoMem(std::string m) : msg(std::move(m)) {}
+  };
+
+ private:
   struct Group {
     int s0 = 0, cap = 0;
     hipStream_t st = nullptr;
@@ -365,52 +487,40 @@ int run(const Job& job, const oi_options& o) {
     std::vector<int> ev_kind;
     std::vector<std::pair<int, int>> ev_meta;
   };
-  std::vector<Group> groups(G);
-  hipEvent_t inputs_ready;
-  HIPC(hipEventCreateWithFlags(&inputs_ready, hipEventDisableTiming));
-  HIPC(hipEventRecord(inputs_ready, st));
-  for (int g = 0; g < G; ++g) {
-    Group& gr = groups[g];
-    gr.s0 = g * capG;
-    gr.cap = std::max(0, std::min(capG, cap - g * capG));
-    gr.st = g == 0 ? st : ctx.aux_stream(g);
-    if (g) HIPC(hipStreamWaitEvent(gr.st, inputs_ready, 0));
-    for (int s = gr.s0 + gr.cap - 1; s >= gr.s0; --s) gr.free_slots.push_back(s);
-    gr.hl = (int32_t*)h_list.p + (size_t)g * capG * 3;
-    gr.dl = (int32_t*)d_list.p + (size_t)g * capG * 3;
-    if (o.profile) {
-      gr.ev.resize(2 * (3 * 1024 + 16));
-      for (auto& ee : gr.ev) HIPC(hipEventCreate(&ee));
-    }
+
+  void release_job(Job* jp) {
+    if (jp->in_off != SIZE_MAX) ctx_.arena.release(jp->in_off, jp->in_bytes);
+    jp->in_off = SIZE_MAX;
+    auto it = jobs_.find(jp->id);
+    if (it != jobs_.end()) jobs_.erase(it);  // frees the job (its own DBuf, if any)
   }
-  double kms[K_COUNT] = {0}, kfl[K_COUNT] = {0};
-  int64_t kln[K_COUNT] = {0};
-  const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
 
-  size_t next = 0;
-  int64_t rounds = 0, evals = 0, predicts = 0;
-
-  auto admit = [&](Group& gr) {
-    while (next < order.size() && !gr.free_slots.empty()) {
-      const int64_t c = order[next];
+  void admit(Group& gr) {
+    while (!queue_.empty() && !gr.free_slots.empty()) {
+      Job* jp = queue_.front().first;
+      const int64_t c = queue_.front().second;
+      const Job& job = *jp;
       const int64_t n = job.offs[c + 1] - job.offs[c];
+      const bool eval_mem = job.kind != Job::PREDICT_ONLY;
       const size_t bytes = cell_bytes(n, eval_mem);
-      const size_t off = ctx.arena.alloc(bytes);
+      const size_t off = ctx_.arena.alloc(bytes);
       if (off == SIZE_MAX) break;
+      queue_.pop_front();
       const int s = gr.free_slots.back();
       gr.free_slots.pop_back();
-      Slot& sl = slots[s];
+      Slot& sl = slots_[s];
       sl = Slot();
+      sl.job = jp;
       sl.cell = c;
       sl.off = off;
       sl.bytes = bytes;
-      if (poison)  // debug: NaN-fill the cell's workspace so any read-before-write shows
-        HIPC(hipMemsetAsync(ctx.arena.ptr(off), 0xFF, bytes, gr.st));
-      OiCell& cd = hc[s];
+      if (poison_)  // debug: NaN-fill the cell's workspace so any read-before-write shows
+        HIPC(hipMemsetAsync(ctx_.arena.ptr(off), 0xFF, bytes, gr.st));
+      OiCell& cd = hc_[s];
       std::memset(&cd, 0, sizeof(cd));
       const int T = tiles_of(n);
       const size_t nt = (size_t)T * (T + 1) / 2;
-      char* p = ctx.arena.ptr(off);
+      char* p = ctx_.arena.ptr(off);
       auto take = [&](size_t x) {
         char* q = p;
         p += (x + 255) & ~size_t(255);
@@ -422,15 +532,14 @@ int run(const Job& job, const oi_options& o) {
       cd.P = take((size_t)T * OI_TILE * 8);
       cd.vec = take(4 * (size_t)T * OI_NB * 8);
       cd.part = take((size_t)OI_PART_SIZE(nt, T) * 8);
-      cd.xyt = d_xyt + 3 * job.offs[c];
-      cd.r = (const double*)d_r.p + job.offs[c];
-      cd.out = (double*)d_res.p + (size_t)s * OI_OUT_N;
-      cd.status = (int32_t*)d_stat.p + s;
+      cd.xyt = job.xyt + 3 * job.offs[c];
+      cd.r = job.r + job.offs[c];
+      cd.out = (double*)d_res_.p + (size_t)s * OI_OUT_N;
+      cd.status = (int32_t*)d_stat_.p + s;
       cd.n = (int32_t)n;
       cd.T = T;
-      if (job.xs) {
+      if (!job.xs.empty())
         for (int d = 0; d < 3; ++d) cd.xs[d] = job.xs[3 * c + d];
-      }
       cd.mean = job.mean;
       if (job.kind == Job::FIT_PREDICT) {
         sl.phase = 0;
@@ -446,16 +555,16 @@ int run(const Job& job, const oi_options& o) {
         for (int k = 0; k < 5; ++k) sl.hyp[k] = std::exp(job.h[6 * c + k]);
       }
       gr.active.push_back(s);
-      ++next;
     }
-  };
+  }
 
-  auto launch_round = [&](Group& gr) {
+  void launch_round(Group& gr) {
     hipStream_t gst = gr.st;
+    OiCell* hc = hc_;
     gr.ev_slots.clear();
     gr.pr_slots.clear();
     for (int s : gr.active) {
-      Slot& sl = slots[s];
+      Slot& sl = slots_[s];
       OiCell& cd = hc[s];
       if (sl.phase == 0) {
         for (int k = 0; k < 5; ++k) cd.hyp[k] = std::exp(sl.mail.x[k]);  // GPR:120-122
@@ -483,8 +592,8 @@ int run(const Job& job, const oi_options& o) {
     const int na = (int)all_slots.size(), ne = (int)gr.ev_slots.size(),
               np_ = (int)gr.pr_slots.size();
     int32_t* l_all = gr.hl;
-    int32_t* l_ev = gr.hl + capG;
-    int32_t* l_pr = gr.hl + 2 * capG;
+    int32_t* l_ev = gr.hl + capG_;
+    int32_t* l_pr = gr.hl + 2 * capG_;
     for (int k = 0; k < na; ++k) l_all[k] = all_slots[k];
     for (int k = 0; k < ne; ++k) l_ev[k] = gr.ev_slots[k];
     for (int k = 0; k < np_; ++k) l_pr[k] = gr.pr_slots[k];
@@ -492,19 +601,20 @@ int run(const Job& job, const oi_options& o) {
     const int maxTe = ne ? hc[gr.ev_slots[0]].T : 0;
     gr.maxT = maxT;
 
-    HIPC(hipMemcpyAsync((OiCell*)d_cells.p + gr.s0, hc + gr.s0, gr.cap * sizeof(OiCell),
+    HIPC(hipMemcpyAsync((OiCell*)d_cells_.p + gr.s0, hc + gr.s0, gr.cap * sizeof(OiCell),
                         hipMemcpyHostToDevice, gst));
-    HIPC(hipMemcpyAsync(gr.dl, gr.hl, (size_t)capG * 4 * 3, hipMemcpyHostToDevice, gst));
-    HIPC(hipMemsetAsync((int32_t*)d_stat.p + gr.s0, 0, gr.cap * 4, gst));
+    HIPC(hipMemcpyAsync(gr.dl, gr.hl, (size_t)capG_ * 4 * 3, hipMemcpyHostToDevice, gst));
+    HIPC(hipMemsetAsync((int32_t*)d_stat_.p + gr.s0, 0, gr.cap * 4, gst));
     const int32_t* dl_all = gr.dl;
-    const int32_t* dl_ev = gr.dl + capG;
-    const int32_t* dl_pr = gr.dl + 2 * capG;
+    const int32_t* dl_ev = gr.dl + capG_;
+    const int32_t* dl_pr = gr.dl + 2 * capG_;
+    const OiCell* dc = dc_;
 
     gr.ev_kind.clear();
     gr.ev_meta.clear();
     int cur_j = -1, cur_cells = 0;
     auto mark = [&](int k, bool end) {
-      if (!o.profile) return;
+      if (!o_.profile) return;
       if (!end) {
         gr.ev_kind.push_back(k);
         gr.ev_meta.emplace_back(cur_j, cur_cells);
@@ -512,6 +622,7 @@ int run(const Job& job, const oi_options& o) {
       const size_t idx = 2 * (gr.ev_kind.size() - 1) + (end ? 1 : 0);
       if (idx < gr.ev.size()) HIPC(hipEventRecord(gr.ev[idx], gst));
     };
+    const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
     int rc = 0;
     cur_cells = na;
     mark(K_BUILD, false);
@@ -525,8 +636,8 @@ int run(const Job& job, const oi_options& o) {
       mark(K_CHOL, false);
       rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, gst);
       mark(K_CHOL, true);
-      const bool even = !legacy && (j % 2 == 0);
-      const int kbeg = (legacy || even) ? 0 : j - 1;
+      const bool even = !legacy_ && (j % 2 == 0);
+      const int kbeg = (legacy_ || even) ? 0 : j - 1;
       mark(K_SCALE, false);
       rc |= oi_launch_scale(dc, dl_all, cnt, j, kbeg, gst);
       mark(K_SCALE, true);
@@ -539,22 +650,22 @@ int run(const Job& job, const oi_options& o) {
         rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, gst);
         mark(K_TRSM, true);
       }
-      if (o.profile) {  // executed MFMA flops: 2*64^3 per 64x64 tile product
+      if (o_.profile) {  // executed MFMA flops: 2*64^3 per 64x64 tile product
         for (int k = 0; k < cnt; ++k) {
           const OiCell& cd = hc[all_slots[k]];
           const bool ev = cd.mode == OI_MODE_EVAL;
-          kfl[K_SCALE] += tf * (double)(j - kbeg);
+          kfl_[K_SCALE] += tf * (double)(j - kbeg);
           if (even) {  // 64x128 blocks: two products per streamed pair
-            kfl[K_EVEN] += tf * 2.0 * (double)(cd.T - 1 - j) * (j + 1);
-            if (cd.T - 1 - j > 0) kfl[K_EVEN] += tf;  // fresh look-ahead product
+            kfl_[K_EVEN] += tf * 2.0 * (double)(cd.T - 1 - j) * (j + 1);
+            if (cd.T - 1 - j > 0) kfl_[K_EVEN] += tf;  // fresh look-ahead product
             if (ev)
-              for (int jj = 0; jj < j; ++jj) kfl[K_EVEN] += tf * 2.0 * (double)(j - jj);
+              for (int jj = 0; jj < j; ++jj) kfl_[K_EVEN] += tf * 2.0 * (double)(j - jj);
           } else {
-            kfl[K_TRSM] += tf * (double)(cd.T - 1 - j) * (j + 1 - kbeg);
-            if (cd.T - 1 - j > 0) kfl[K_TRSM] += tf * (double)(j + 1);  // look-ahead diagonal
+            kfl_[K_TRSM] += tf * (double)(cd.T - 1 - j) * (j + 1 - kbeg);
+            if (cd.T - 1 - j > 0) kfl_[K_TRSM] += tf * (double)(j + 1);  // look-ahead diagonal
             if (ev)
               for (int jj = 0; jj < j; ++jj)
-                kfl[K_TRSM] += tf * (double)(j - std::max(jj, kbeg) + (kbeg > jj ? 1 : 0));
+                kfl_[K_TRSM] += tf * (double)(j - std::max(jj, kbeg) + (kbeg > jj ? 1 : 0));
           }
         }
       }
@@ -578,38 +689,37 @@ int run(const Job& job, const oi_options& o) {
     rc |= oi_launch_predict(dc, dl_pr, np_, gst);
     mark(K_PRED, true);
     if (rc) throw HipError(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    HIPC(hipMemcpyAsync(hres + (size_t)gr.s0 * OI_OUT_N, (double*)d_res.p + (size_t)gr.s0 * OI_OUT_N,
+    HIPC(hipMemcpyAsync(hres_ + (size_t)gr.s0 * OI_OUT_N, (double*)d_res_.p + (size_t)gr.s0 * OI_OUT_N,
                         (size_t)gr.cap * OI_OUT_N * 8, hipMemcpyDeviceToHost, gst));
-    HIPC(hipMemcpyAsync(hst + gr.s0, (int32_t*)d_stat.p + gr.s0, (size_t)gr.cap * 4,
+    HIPC(hipMemcpyAsync(hst_ + gr.s0, (int32_t*)d_stat_.p + gr.s0, (size_t)gr.cap * 4,
                         hipMemcpyDeviceToHost, gst));
-    if (o.profile) {
+    if (o_.profile) {
       for (int k = 0; k < ne; ++k) {
         const OiCell& cd = hc[gr.ev_slots[k]];
-        for (int i = 0; i < cd.T; ++i) kfl[K_LAUUM] += tf * (double)(cd.T - i) * (i + 1);
+        for (int i = 0; i < cd.T; ++i) kfl_[K_LAUUM] += tf * (double)(cd.T - i) * (i + 1);
       }
     }
     gr.inflight = true;
-  };
+  }
 
-  double sync_s = 0.0;
-  auto consume = [&](Group& gr) {
+  void consume(Group& gr) {
     const auto ts0 = std::chrono::steady_clock::now();
     HIPC(hipStreamSynchronize(gr.st));
-    sync_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts0).count();
+    sync_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts0).count();
     gr.inflight = false;
-    ++rounds;
-    if (o.profile) {
+    ++rounds_;
+    if (o_.profile) {
       std::vector<LaunchRec> recs;
       for (size_t q = 0; q < gr.ev_kind.size() && 2 * q + 1 < gr.ev.size(); ++q) {
         float a = 0;
         HIPC(hipEventElapsedTime(&a, gr.ev[2 * q], gr.ev[2 * q + 1]));
-        kms[gr.ev_kind[q]] += a;
-        kln[gr.ev_kind[q]]++;
+        kms_[gr.ev_kind[q]] += a;
+        kln_[gr.ev_kind[q]]++;
         recs.push_back({gr.ev_kind[q], gr.ev_meta[q].first, gr.ev_meta[q].second, (double)a});
       }
       double rms = 0.0, work = 0.0;
       for (const auto& rr : recs) rms += rr.ms;
-      for (int s : gr.ev_slots) work += std::pow((double)hc[s].T, 3.0);
+      for (int s : gr.ev_slots) work += std::pow((double)hc_[s].T, 3.0);
       std::lock_guard<std::mutex> pl(g_prof_mu);
       g_last_round.swap(recs);
       g_rounds.push_back({(int)gr.ev_slots.size(), (int)gr.pr_slots.size(), gr.maxT, work, rms});
@@ -617,12 +727,13 @@ int run(const Job& job, const oi_options& o) {
     std::vector<int> still;
     still.reserve(gr.active.size());
     for (int s : gr.active) {
-      Slot& sl = slots[s];
-      const double* rr = hres + (size_t)s * OI_OUT_N;
+      Slot& sl = slots_[s];
+      Job& job = *sl.job;
+      const double* rr = hres_ + (size_t)s * OI_OUT_N;
       const int64_t c = sl.cell;
       bool done = false;
       if (sl.phase == 0) {
-        ++evals;
+        ++evals_;
         sl.mail.f = rr[0];
         for (int k = 0; k < oi::NH; ++k) sl.mail.g[k] = rr[1 + k];
         sl.mail.pending = false;
@@ -633,22 +744,22 @@ int run(const Job& job, const oi_options& o) {
           for (int k = 0; k < 5; ++k) sl.hyp[k] = std::exp(sl.res.x[k]);  // GPR:166-168
         }
       } else if (sl.phase == 2) {
-        ++evals;
+        ++evals_;
         job.nlz[c] = rr[0];
         for (int k = 0; k < oi::NH; ++k) job.grad[6 * c + k] = rr[1 + k];
-        if (job.status) job.status[c] = hst[s];
+        if (job.status) job.status[c] = hst_[s];
         done = true;
       } else {
-        ++predicts;
+        ++predicts_;
         double* dst = job.out + 8 * c;
         dst[0] = rr[0];
         dst[1] = rr[1];
         dst[2] = rr[2];
         for (int k = 0; k < 5; ++k) dst[3 + k] = sl.hyp[k];
-        if (hst[s] != OI_OK) {
+        if (hst_[s] != OI_OK) {
           for (int k = 0; k < 8; ++k) dst[k] = NAN;  // GPR:187-189
         }
-        if (job.status) job.status[c] = hst[s];
+        if (job.status) job.status[c] = hst_[s];
         if (job.info) {
           int32_t* inf = job.info + 4 * c;
           inf[0] = sl.res.nit;
@@ -659,59 +770,62 @@ int run(const Job& job, const oi_options& o) {
         done = true;
       }
       if (done) {
-        ctx.arena.release(sl.off, sl.bytes);
+        ctx_.arena.release(sl.off, sl.bytes);
         sl.task = oi::Task<oi::CgResult>();
         sl.cell = -1;
+        sl.job = nullptr;
         gr.free_slots.push_back(s);
+        if (--job.remaining == 0) release_job(&job);
       } else {
         still.push_back(s);
       }
     }
     gr.active.swap(still);
-  };
+  }
 
-  const double setup_s =
-      std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-  while (true) {
-    bool any = false;
-    for (Group& gr : groups) {
-      if (gr.inflight) consume(gr);
-      admit(gr);
-      if (!gr.active.empty()) {
-        launch_round(gr);
-        any = true;
+  void flush_stats() {
+    std::lock_guard<std::mutex> pl(g_prof_mu);
+    if (o_.profile) {
+      for (int k = 0; k < K_COUNT; ++k) {
+        g_prof[k].launches += kln_[k];
+        g_prof[k].ms += kms_[k];
+        g_prof[k].flops += kfl_[k];
+        kln_[k] = 0;
+        kms_[k] = kfl_[k] = 0.0;
       }
     }
-    if (!any) {
-      if (next < order.size()) return fail(OI_E_NOMEM, "workspace exhausted with no resident cell");
-      break;
-    }
+    g_run.rounds += rounds_;
+    g_run.evals += evals_;
+    g_run.predicts += predicts_;
+    g_run.sync_s += sync_s_;
+    g_run.wall_s += wall_s_;
+    rounds_ = evals_ = predicts_ = 0;
+    sync_s_ = wall_s_ = 0.0;
   }
-  (void)hipEventDestroy(inputs_ready);
-  if (o.profile) {
-    for (Group& gr : groups)
-      for (auto& ee : gr.ev) (void)hipEventDestroy(ee);
-  }
-  if (o.profile) {
-    std::lock_guard<std::mutex> pl(g_prof_mu);
-    for (int k = 0; k < K_COUNT; ++k) {
-      g_prof[k].launches += kln[k];
-      g_prof[k].ms += kms[k];
-      g_prof[k].flops += kfl[k];
-    }
-  }
-  {
-    std::lock_guard<std::mutex> pl(g_prof_mu);
-    g_run.rounds += rounds;
-    g_run.evals += evals;
-    g_run.predicts += predicts;
-    g_run.setup_s += setup_s;
-    g_run.sync_s += sync_s;
-    g_run.wall_s +=
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-  }
-  return 0;
-}
+
+  Context& ctx_;
+  oi_options o_;
+  bool legacy_ = false, poison_ = false;
+  hipStream_t st_ = nullptr;
+  hipEvent_t ready_ = nullptr;
+  int cap_ = 1, G_ = 1, capG_ = 1;
+  std::vector<Slot> slots_;
+  std::vector<Group> groups_;
+  DBuf d_cells_, d_list_, d_res_, d_stat_;
+  HBuf h_cells_, h_list_, h_res_, h_stat_;
+  OiCell* hc_ = nullptr;
+  const OiCell* dc_ = nullptr;
+  double* hres_ = nullptr;
+  int32_t* hst_ = nullptr;
+  std::deque<std::pair<Job*, int64_t>> queue_;
+  std::map<int64_t, std::unique_ptr<Job>> jobs_;
+  int64_t next_id_ = 0;
+  double kms_[K_COUNT] = {0}, kfl_[K_COUNT] = {0};
+  int64_t kln_[K_COUNT] = {0};
+  int64_t rounds_ = 0, evals_ = 0, predicts_ = 0;
+  double sync_s_ = 0.0, wall_s_ = 0.0;
+  std::chrono::steady_clock::time_point t_start_;
+};
 
 bool check_offs(const int64_t* offs, int64_t ncell) {
   if (!offs || offs[0] != 0) return false;
@@ -720,18 +834,69 @@ bool check_offs(const int64_t* offs, int64_t ncell) {
   return true;
 }
 
-int guarded(const Job& job, const oi_options* opts) {
+oi_options resolve(const oi_options* opts) {
   oi_options o;
   oi_options_default(&o);
   if (opts) o = *opts;
+  return o;
+}
+
+int check_device(const oi_options& o) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(OI_E_NODEV, "no HIP device available");
+  if (o.device < 0 || o.device >= ndev) return fail(OI_E_ARG, "bad device ordinal");
+  return 0;
+}
+
+// Validates the oi_gpr_batch arguments and fills a Job (host metadata copied).
+int make_gpr_job(const double* xyt, const double* z, const int64_t* offs, int64_t ncell,
+                 const double* xs, double mean, const double* x0, int32_t opt, const double* hyp,
+                 double* out, int32_t* status, int32_t* info, const oi_options& o,
+                 std::unique_ptr<Job>& job) {
+  if (ncell < 0 || !check_offs(offs, ncell)) return fail(OI_E_ARG, "bad offs / ncell");
+  const int64_t N = ncell ? offs[ncell] : 0;
+  if (ncell > 0 && ((N > 0 && (!xyt || !z)) || !xs || !out)) return fail(OI_E_ARG, "null input/output pointer");
+  if (opt && !x0) return fail(OI_E_ARG, "opt=1 needs x0");
+  if (!opt && !hyp) return fail(OI_E_ARG, "opt=0 needs hyp");
+  job = std::make_unique<Job>();
+  Job& jb = *job;
+  jb.offs.assign(offs, offs + ncell + 1);
+  jb.ncell = ncell;
+  if (ncell > 0) jb.xs.assign(xs, xs + 3 * ncell);
+  jb.mean = mean;  // outputs - mX with mX = ones(n)*mean  (GPR:163, GPR:178)
+  jb.kind = opt ? Job::FIT_PREDICT : Job::PREDICT_ONLY;
+  if (opt) jb.x0.assign(x0, x0 + 6);
+  else jb.hyp.assign(hyp, hyp + 5 * ncell);
+  jb.cg.gtol = o.gtol;
+  jb.cg.maxiter = o.maxiter;
+  jb.out = out;
+  jb.status = status;
+  jb.info = info;
+  return 0;
+}
+
+// One-shot batch: a private engine, submit + drain.
+int run_once(std::unique_ptr<Job> job, const double* xyt, const double* y, const double* mX,
+             const oi_options& o) {
   try {
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-      return fail(OI_E_NODEV, "no HIP device available");
-    if (o.device < 0 || o.device >= ndev) return fail(OI_E_ARG, "bad device ordinal");
-    return run(job, o);
+    if (int rc = check_device(o)) return rc;
+    if (job->ncell == 0) return 0;
+    Context& ctx = context(o.device, o.pool_bytes);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    const auto t0 = std::chrono::steady_clock::now();
+    Engine eng(ctx, o, job->ncell);
+    eng.submit(std::move(job), xyt, y, mX);
+    const double setup = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    {
+      std::lock_guard<std::mutex> pl(g_prof_mu);
+      g_run.setup_s += setup;
+    }
+    eng.wait(-1);
+    return 0;
   } catch (const HipError& e) {
     return fail(OI_E_HIP, e.msg);
+  } catch (const Engine::NoMem& e) {
+    return fail(OI_E_NOMEM, e.msg);
   } catch (const std::bad_alloc&) {
     return fail(OI_E_NOMEM, "host allocation failed");
   }
@@ -760,30 +925,11 @@ int oi_gpr_batch(const double* xyt, const double* z, const int64_t* offs, int64_
                  double* out, int32_t* status, int32_t* info, const oi_options* opts) {
   if (ncell < 0 || !check_offs(offs, ncell)) return fail(OI_E_ARG, "bad offs / ncell");
   if (ncell == 0) return 0;
-  const int64_t N = offs[ncell];
-  if ((N > 0 && (!xyt || !z)) || !xs || !out) return fail(OI_E_ARG, "null input/output pointer");
-  if (opt && !x0) return fail(OI_E_ARG, "opt=1 needs x0");
-  if (!opt && !hyp) return fail(OI_E_ARG, "opt=0 needs hyp");
-  Job job;
-  job.xyt = xyt;
-  job.offs = offs;
-  job.ncell = ncell;
-  job.y = z;  // outputs - mX with mX = ones(n)*mean  (GPR:163, GPR:178)
-  job.mX = nullptr;
-  job.xs = xs;
-  job.mean = mean;
-  job.kind = opt ? Job::FIT_PREDICT : Job::PREDICT_ONLY;
-  job.x0 = x0;
-  job.hyp = hyp;
-  oi_options o;
-  oi_options_default(&o);
-  if (opts) o = *opts;
-  job.cg.gtol = o.gtol;
-  job.cg.maxiter = o.maxiter;
-  job.out = out;
-  job.status = status;
-  job.info = info;
-  return guarded(job, &o);
+  const oi_options o = resolve(opts);
+  std::unique_ptr<Job> job;
+  if (int rc = make_gpr_job(xyt, z, offs, ncell, xs, mean, x0, opt, hyp, out, status, info, o, job))
+    return rc;
+  return run_once(std::move(job), xyt, z, nullptr, o);
 }
 
 int oi_nlml_grad_batch(const double* xyt, const double* y, const double* mX, const int64_t* offs,
@@ -794,18 +940,94 @@ int oi_nlml_grad_batch(const double* xyt, const double* y, const double* mX, con
   const int64_t N = offs[ncell];
   if ((N > 0 && (!xyt || !y || !mX)) || !h || !nlz || !grad)
     return fail(OI_E_ARG, "null input/output pointer");
-  Job job;
-  job.xyt = xyt;
-  job.offs = offs;
-  job.ncell = ncell;
-  job.y = y;
-  job.mX = mX;  // y - mX, GPR:127
-  job.kind = Job::EVAL_ONLY;
-  job.h = h;
-  job.nlz = nlz;
-  job.grad = grad;
-  job.status = status;
-  return guarded(job, opts);
+  auto job = std::make_unique<Job>();
+  job->offs.assign(offs, offs + ncell + 1);
+  job->ncell = ncell;
+  job->kind = Job::EVAL_ONLY;  // y - mX, GPR:127
+  job->h.assign(h, h + 6 * ncell);
+  job->nlz = nlz;
+  job->grad = grad;
+  job->status = status;
+  return run_once(std::move(job), xyt, y, mX, resolve(opts));
+}
+
+// ---- session: continuous batching across calls
+struct oi_session {
+  oi_options o;
+  Context* ctx = nullptr;
+  std::unique_ptr<Engine> eng;
+};
+
+oi_session* oi_session_create(const oi_options* opts) {
+  const oi_options o = resolve(opts);
+  try {
+    if (check_device(o)) return nullptr;
+    auto* s = new oi_session();
+    s->o = o;
+    s->ctx = &context(o.device, o.pool_bytes);
+    std::lock_guard<std::mutex> lk(s->ctx->mu);
+    s->eng = std::make_unique<Engine>(*s->ctx, o, INT64_MAX);
+    s->ctx->live_sessions++;
+    return s;
+  } catch (const HipError& e) {
+    fail(OI_E_HIP, e.msg);
+  } catch (const std::bad_alloc&) {
+    fail(OI_E_NOMEM, "host allocation failed");
+  }
+  return nullptr;
+}
+
+int64_t oi_session_submit(oi_session* s, const double* xyt, const double* z, const int64_t* offs,
+                          int64_t ncell, const double* xs, double mean, const double* x0, int32_t opt,
+                          const double* hyp, double* out, int32_t* status, int32_t* info) {
+  if (!s) return fail(OI_E_ARG, "null session");
+  std::unique_ptr<Job> job;
+  if (int rc = make_gpr_job(xyt, z, offs, ncell, xs, mean, x0, opt, hyp, out, status, info, s->o, job))
+    return rc;
+  try {
+    std::lock_guard<std::mutex> lk(s->ctx->mu);
+    HIPC(hipSetDevice(s->o.device));
+    return s->eng->submit(std::move(job), xyt, z, nullptr);
+  } catch (const HipError& e) {
+    return fail(OI_E_HIP, e.msg);
+  } catch (const Engine::NoMem& e) {
+    return fail(OI_E_NOMEM, e.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(OI_E_NOMEM, "host allocation failed");
+  }
+}
+
+int oi_session_wait(oi_session* s, int64_t ticket) {
+  if (!s) return fail(OI_E_ARG, "null session");
+  try {
+    std::lock_guard<std::mutex> lk(s->ctx->mu);
+    HIPC(hipSetDevice(s->o.device));
+    s->eng->wait(ticket < 0 ? -1 : ticket);
+    return 0;
+  } catch (const HipError& e) {
+    return fail(OI_E_HIP, e.msg);
+  } catch (const Engine::NoMem& e) {
+    return fail(OI_E_NOMEM, e.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(OI_E_NOMEM, "host allocation failed");
+  }
+}
+
+int oi_session_done(oi_session* s, int64_t ticket) {
+  if (!s) return fail(OI_E_ARG, "null session");
+  std::lock_guard<std::mutex> lk(s->ctx->mu);
+  return s->eng->done(ticket) ? 1 : 0;
+}
+
+void oi_session_destroy(oi_session* s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> lk(s->ctx->mu);
+    (void)hipSetDevice(s->o.device);
+    s->eng.reset();
+    s->ctx->live_sessions--;
+  }
+  delete s;
 }
 
 // ---- optimiser handle

@@ -16,7 +16,8 @@ neighbour query (``oi_ball_query``) and the per-cell gather
 the five smoothings are one ``oi_smooth_fields`` call, and the only
 collectives are one all_gather of the pass-1 rows (every rank then smooths
 the same fields itself -- replacing gather + rank-0 smooth + bcast) and one
-gather of the pass-2 rows to rank 0.
+gather of the pass-2 rows to rank 0 (driver.gather_rows: the partition is
+known on every rank, so each exchange is a single collective).
 
 ``neighbours='kdtree'`` keeps the reference's exact neighbour order (scipy
 cKDTree on the host, rows shipped over PCIe); the default ``'device'``
@@ -157,32 +158,6 @@ def write_quicklook(path, fs, sd, x=None, y=None, lat=None, lon=None):
             v[:] = np.asarray(arr, dtype=np.float64)
 
 
-def _allgather_rows(rows, mine, ncell, device, group=None):
-    """Every rank gets the full ncell x m array (one all_gather of the padded
-    payload after one all_gather of the sizes)."""
-    import torch
-    import torch.distributed as dist
-    m = rows.shape[1]
-    world = dist.get_world_size(group)
-    k = torch.tensor([len(mine)], dtype=torch.int64, device=device)
-    ks = [torch.zeros_like(k) for _ in range(world)]
-    dist.all_gather(ks, k, group=group)
-    kmax = max(int(x.item()) for x in ks)
-    full = np.full((ncell, m), np.nan)
-    if kmax == 0:  # every rank empty (e.g. a day without ice): no payload to exchange
-        return full
-    pay = torch.zeros((kmax, m + 1), dtype=torch.float64, device=device)
-    if len(mine):
-        pay[:len(mine), 0] = torch.from_numpy(np.asarray(mine, dtype=np.float64))
-        pay[:len(mine), 1:] = torch.from_numpy(rows)
-    bufs = [torch.zeros_like(pay) for _ in range(world)]
-    dist.all_gather(bufs, pay, group=group)
-    for r in range(world):
-        b = bufs[r][:int(ks[r].item())].cpu().numpy()
-        full[b[:, 0].astype(np.int64)] = b[:, 1:]
-    return full
-
-
 class DayResult(dict):
     """The reference's output dict (GPR:290-307, 333-334) plus run info."""
     info = None
@@ -238,6 +213,7 @@ def _prepare_day(sat, sie, mean, date, x, y, T, rad, neighbours, rank, world, de
         parts = driver.lpt_partition(driver.cell_costs(d.counts, opt=not fixed), world)
     else:
         parts = [np.asarray(p, dtype=np.int64) for p in split(np.arange(d.ncell), world)]
+    d.parts = parts
     d.mine = parts[rank]
     if neighbours == 'device':
         q = qall[torch.from_numpy(d.mine).to(dev)] if len(d.mine) else qall[:0]
@@ -330,7 +306,7 @@ def interpolate_days(days, x, y, T=9, radius=300, grid_res=25, x0=None, neighbou
         rows1, info1 = p1[id(d)]
         payload = np.column_stack([rows1, info1]) if len(d.mine) else np.zeros((0, 12))
         if world > 1:
-            d.full = _allgather_rows(payload, d.mine, d.ncell, cdev, group)
+            d.full = driver.gather_rows(payload, d.parts, d.ncell, device=cdev, group=group, to_all=True)
         else:
             d.full = np.full((d.ncell, 12), np.nan)
             d.full[d.mine] = payload
@@ -358,7 +334,7 @@ def interpolate_days(days, x, y, T=9, radius=300, grid_res=25, x0=None, neighbou
     for d, res in zip(D, results):
         rows2 = p2[id(d)][0][:, :2]
         if world > 1:
-            full2 = driver.gather_rows(rows2, d.mine, d.ncell, device=cdev, group=group)
+            full2 = driver.gather_rows(rows2, d.parts, d.ncell, device=cdev, group=group)
             if rank != 0:
                 out.append(None)
                 continue

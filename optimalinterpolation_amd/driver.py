@@ -6,7 +6,8 @@ per-cell tuples back to rank 0 (``COMM.gather`` :262).  Here: one process per
 GPU; cells are partitioned by longest-processing-time-first on an n^3 cost
 estimate (or the reference's strided split); every rank runs its cells through
 one batched liboi call; the ncell x 8 fp64 results come back to rank 0 in one
-collective (RCCL over xGMI on GPUs, gloo in CPU tests).  There is no other
+collective -- a single ``gather`` (every rank computes the same partition, so
+no size exchange is needed), RCCL over xGMI on GPUs, gloo in CPU tests.  There is no other
 data-path communication: cells are independent.
 """
 import numpy as np
@@ -39,35 +40,43 @@ def cell_costs(sizes, opt=True):
     return (85.0 + 0.045 * np.maximum(n - 300.0, 0.0)) * (n ** 3 + 40 * n ** 2) + 1.0
 
 
-def gather_rows(local_rows, local_idx, ncell, device=None, group=None):
-    """Gather per-cell result rows from every rank to rank 0 (one all_gather of
-    sizes + one all_gather of the padded [idx | rows] payload).  Returns the
-    full (ncell x m) array on rank 0 (rows in global cell order), None elsewhere."""
+def gather_rows(local_rows, parts, ncell, device=None, group=None, to_all=False):
+    """The single collective of a sharded pass (GPR:262 / GPR:320 ``COMM.gather``):
+    rank r holds the rows of cells ``parts[r]``; the partition is computed
+    identically on every rank, so the sizes are known everywhere and one
+    ``gather`` to rank 0 of the [kmax x m] padded rows suffices (``to_all``:
+    one ``all_gather``, every rank gets the table -- the pass-1 exchange that
+    replaces gather + bcast, GPR:262/311).  Over RCCL the payload stays on
+    ``device``.  Returns the (ncell x m) table in global cell order on rank 0
+    (every rank with ``to_all``), None elsewhere."""
     import torch
     import torch.distributed as dist
     local_rows = np.asarray(local_rows, dtype=np.float64)
-    m = local_rows.shape[1] if local_rows.ndim == 2 else 0
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    k = torch.tensor([len(local_idx)], dtype=torch.int64, device=device)
-    ks = [torch.zeros_like(k) for _ in range(world)]
-    dist.all_gather(ks, k, group=group)
-    kmax = int(max(int(x.item()) for x in ks))
-    if kmax == 0:  # every rank empty: nothing to exchange
-        return np.full((ncell, m), np.nan) if rank == 0 else None
-    pay = torch.zeros((kmax, m + 1), dtype=torch.float64, device=device)
-    if len(local_idx):
-        pay[:len(local_idx), 0] = torch.from_numpy(np.asarray(local_idx, dtype=np.float64))
-        pay[:len(local_idx), 1:] = torch.from_numpy(local_rows)
-    bufs = [torch.zeros_like(pay) for _ in range(world)]
-    dist.all_gather(bufs, pay, group=group)
-    if rank != 0:
-        return None
+    m = local_rows.shape[1] if local_rows.ndim == 2 else 0
+    counts = [len(p) for p in parts]
+    if len(parts) != world or counts[rank] != local_rows.shape[0]:
+        raise ValueError("partition does not match the process group / local rows")
+    kmax = max(counts) if counts else 0
     full = np.full((ncell, m), np.nan)
+    if kmax == 0:  # every rank empty (e.g. a day without ice): nothing to exchange
+        return full if (to_all or rank == 0) else None
+    pay = torch.zeros((kmax, m), dtype=torch.float64, device=device)
+    if counts[rank]:
+        pay[:counts[rank]] = torch.from_numpy(local_rows).to(pay.device)
+    if to_all:
+        bufs = [torch.empty_like(pay) for _ in range(world)]
+        dist.all_gather(bufs, pay, group=group)
+    else:
+        bufs = [torch.empty_like(pay) for _ in range(world)] if rank == 0 else None
+        dist.gather(pay, bufs, dst=dist.get_global_rank(group, 0) if group is not None else 0,
+                    group=group)
+        if rank != 0:
+            return None
     for r in range(world):
-        kr = int(ks[r].item())
-        b = bufs[r][:kr].cpu().numpy()
-        full[b[:, 0].astype(np.int64)] = b[:, 1:]
+        if counts[r]:
+            full[np.asarray(parts[r], dtype=np.int64)] = bufs[r][:counts[r]].cpu().numpy()
     return full
 
 
@@ -91,7 +100,7 @@ def run_sharded(cells, compute, rank, world, device=None, partition='lpt', opt=T
         rows = np.column_stack([out, status.astype(np.float64), info.astype(np.float64)])
     else:
         rows = np.zeros((0, 13))
-    return gather_rows(rows, mine, cells.ncell, device=device, group=group)
+    return gather_rows(rows, parts, cells.ncell, device=device, group=group)
 
 
 def gpu_compute(opt=True, x0=None, hyp=None, **kw):

@@ -84,14 +84,14 @@ def _allgather_worker(rank, world, port, q):
     parts = day.split(np.arange(ncell), world)
     mine = parts[rank]
     rows = np.column_stack([mine * 10.0, mine + 0.5])
-    full = day._allgather_rows(rows, mine, ncell, device='cpu')
+    full = driver.gather_rows(rows, parts, ncell, device='cpu', to_all=True)
     q.put((rank, full))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_day_allgather_every_rank_gets_all_rows():
-    """The day pipeline's single pass-1 exchange (day._allgather_rows): every
+    """The day pipeline's single pass-1 exchange (driver.gather_rows, to_all): every
     rank ends with the full ncell x m table (it then smooths locally)."""
     world = 2
     ctx = mp.get_context('spawn')

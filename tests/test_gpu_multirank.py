@@ -1,0 +1,117 @@
+"""Config 4's code path on the real HIP library: two ranks (one process each)
+sharing cuda:0, collectives over gloo on the host (the 1-GPU box cannot run
+RCCL between two processes on one device).  The reference distributes cells
+over MPI ranks (split GPR:18-23, scatter GPR:256) and gathers per-cell tuples
+(GPR:262, GPR:320); cells are independent and per-cell arithmetic never
+depends on the batch, so the sharded results must equal the single-rank
+call BITWISE:
+  * driver.run_sharded(..., driver.gpu_compute())  (pass 1, LPT partition)
+  * day.interpolate_day(world=2)                   (two-pass day pipeline:
+    device neighbour query, pass 1, all_gather, smoothing, pass 2, gather)
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+X0 = np.array([np.log(25e3), np.log(25e3), 0.0, 0.0, 0.0, np.log(.1)])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cells():
+    from optimalinterpolation_amd import synthetic
+    return synthetic.make_cells(np.random.default_rng(3).integers(30, 260, 300), seed=17)
+
+
+def _binned_day():
+    from optimalinterpolation_amd import synthetic
+    return synthetic.make_binned_day(seed=8, nx=40, ice_radius_m=120e3, obs_radius_m=450e3,
+                                     cover=(0.02, 0.05))
+
+
+def _worker(rank, world, port, q, logpath):
+    import faulthandler
+    import traceback
+    log = open(logpath, 'a', buffering=1)
+    faulthandler.dump_traceback_later(60, repeat=False, file=log)  # where a hung rank sits
+    try:
+        import torch
+        import torch.distributed as dist
+        from optimalinterpolation_amd import day, driver
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        log.write(f"rank {rank}: process group up\n")
+        torch.cuda.set_device(0)
+        full = driver.run_sharded(_cells(), driver.gpu_compute(opt=True, x0=X0, device=0), rank, world)
+        log.write(f"rank {rank}: run_sharded done\n")
+        d = _binned_day()
+        res = day.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='d', rank=rank, world=world,
+                                  device=0, comm_device=torch.device('cpu'))
+        log.write(f"rank {rank}: interpolate_day done\n")
+        q.put((rank, full, None if res is None else {k: np.asarray(v) for k, v in res.items()}, None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        q.put((rank, None, None, traceback.format_exc()))
+        raise
+
+
+def test_two_ranks_equal_one_rank_bitwise(tmp_path):
+    import queue
+    import time
+    from optimalinterpolation_amd import _lib, day
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    logpath = str(tmp_path / 'ranks.log')
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, logpath)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    deadline = time.time() + 150
+    try:
+        while len(got) < world:
+            try:
+                r, full, res, err = q.get(timeout=2)
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                log = open(logpath).read() if os.path.exists(logpath) else ''
+                assert not dead and time.time() < deadline, f"ranks failed/hung: exit {dead}\n{log}"
+                continue
+            assert err is None, f"rank {r} raised:\n{err}"
+            got[r] = (full, res)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert got[1][0] is None and got[1][1] is None  # only rank 0 holds the gathered results
+    full, res = got[0]
+    # single rank, same library, same cells
+    cells = _cells()
+    out, st, info = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, x0=X0, opt=True,
+                                   info=True)
+    assert full.shape == (cells.ncell, 13)
+    assert np.array_equal(full[:, :8], out, equal_nan=True)
+    assert np.array_equal(full[:, 8], st.astype(float))
+    assert np.array_equal(full[:, 9:], info.astype(float))
+    d = _binned_day()
+    ref = day.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date='d')
+    assert set(res) == set(ref)
+    for k in ref:
+        assert np.array_equal(res[k], np.asarray(ref[k]), equal_nan=True), k

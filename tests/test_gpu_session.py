@@ -1,0 +1,99 @@
+"""The continuous-batching session (oi_session_*, include/oi.h) on the GPU.
+
+A stream of batches through one session must give, cell for cell, bitwise
+the results of one oi_gpr_batch call over the same cells (per-cell arithmetic
+never depends on which cells share a round), for fits (GPR3D opt=True,
+GPR:143-191) and predict-only batches (opt=False, GPR:170-182), with host and
+device inputs, whatever the order of submit / wait calls.
+"""
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as O
+from optimalinterpolation_amd import _lib, synthetic
+
+pytestmark = pytest.mark.gpu
+
+X0 = np.array(O.X0_PRODUCTION)
+
+
+def _slices(cells, k):
+    edges = np.linspace(0, cells.ncell, k + 1).astype(int)
+    return [cells.subset(np.arange(a, b)) for a, b in zip(edges[:-1], edges[1:])]
+
+
+def test_session_fit_equals_one_call():
+    cells = synthetic.make_cells([0, 1, 40, 70, 130, 200, 64, 65, 333, 90, 17, 250], seed=41)
+    ref, rst, rinf = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, x0=X0, opt=True,
+                                    info=True)
+    parts = _slices(cells, 4)
+    with _lib.Session() as s:
+        tickets = [s.submit(p.xyt, p.z, p.offs, p.xs, p.mean, x0=X0) for p in parts]
+        # wait out of order: the last batch first, then the rest
+        res = {3: s.wait(tickets[3])}
+        for k in (1, 0, 2):
+            res[k] = s.wait(tickets[k])
+    out = np.concatenate([res[k][0] for k in range(4)])
+    st = np.concatenate([res[k][1] for k in range(4)])
+    inf = np.concatenate([res[k][2] for k in range(4)])
+    assert np.array_equal(out, ref, equal_nan=True)
+    assert np.array_equal(st, rst)
+    assert np.array_equal(inf, rinf)
+
+
+def test_session_pipelined_device_inputs():
+    import torch
+    cells = synthetic.make_cells(np.random.default_rng(5).integers(50, 400, 24), seed=43)
+    ref, _, rinf = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, x0=X0, opt=True,
+                                  info=True)
+    parts = _slices(cells, 6)
+    dev = [(torch.from_numpy(p.xyt).cuda(), torch.from_numpy(p.z).cuda()) for p in parts]
+    outs = {}
+    with _lib.Session(device_inputs=True, profile=True) as s:
+        t = []
+        for k, p in enumerate(parts):  # the bench's depth-1 pipeline
+            t.append(s.submit(dev[k][0], dev[k][1], p.offs, p.xs, p.mean, x0=X0))
+            if k >= 1:
+                outs[k - 1] = s.wait(t[k - 1])
+        outs[len(parts) - 1] = s.wait(t[-1])
+        assert all(s.done(x) for x in t)
+    out = np.concatenate([outs[k][0] for k in range(len(parts))])
+    inf = np.concatenate([outs[k][2] for k in range(len(parts))])
+    assert np.array_equal(out, ref)
+    assert np.array_equal(inf, rinf)
+
+
+def test_session_predict_and_fit_mixed():
+    cells = synthetic.make_cells([100, 260, 30, 500, 0, 75], seed=47)
+    hyp = np.tile(synthetic.FIXED_HYPERS, (cells.ncell, 1))
+    rp, _, _ = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+    rf, _, _ = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, x0=X0, opt=True)
+    with _lib.Session() as s:
+        a = s.submit(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+        b = s.submit(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, x0=X0)
+        e = s.submit(np.zeros((0, 3)), np.zeros(0), [0], np.zeros((0, 3)), cells.mean, x0=X0)
+        assert s.done(e)  # an empty batch completes at once
+        pb = s.wait(b)
+        pa = s.wait(a)
+        s.wait(-1)
+    assert np.array_equal(pa[0], rp, equal_nan=True)
+    assert np.array_equal(pb[0], rf, equal_nan=True)
+    for k in range(cells.ncell):  # T1 against the oracle (GPR:173-182)
+        x, y, xs = cells.cell(k)
+        if len(y) == 0:
+            continue
+        fs, sd, lZ = O.predict(x, y, xs, cells.mean, synthetic.FIXED_HYPERS[:3], synthetic.FIXED_HYPERS[3],
+                               synthetic.FIXED_HYPERS[4])
+        assert abs(pa[0][k, 0] - fs[0]) <= 1e-10 * max(1, abs(fs[0]))
+        assert abs(pa[0][k, 1] - sd[0]) <= 1e-10 * max(1, abs(sd[0]))
+
+
+def test_device_input_checks():
+    import torch
+    cells = synthetic.make_cells([20], seed=1)
+    with pytest.raises(ValueError, match='float64'):
+        _lib.gpr_batch_device(torch.from_numpy(cells.xyt).float().cuda(), torch.from_numpy(cells.z).cuda(),
+                              cells.offs, cells.xs, cells.mean, x0=X0)
+    with pytest.raises(ValueError, match='cuda'):
+        _lib.gpr_batch_device(torch.from_numpy(cells.xyt), torch.from_numpy(cells.z).cuda(),
+                              cells.offs, cells.xs, cells.mean, x0=X0)
