@@ -1030,67 +1030,6 @@ void oi_session_destroy(oi_session* s) {
   delete s;
 }
 
-// ---- optimiser handle
-struct oi_cg {
-  oi::EvalSlot mail;
-  oi::Task<oi::CgResult> task;
-  bool started = false;
-};
-
-oi_cg* oi_cg_create(const double* x0, double gtol, int32_t maxiter) {
-  if (!x0) {
-    fail(OI_E_ARG, "null x0");
-    return nullptr;
-  }
-  auto* h = new oi_cg();
-  oi::Vec v;
-  for (int k = 0; k < oi::NH; ++k) v[k] = x0[k];
-  oi::CgOptions o;
-  o.gtol = gtol;
-  o.maxiter = maxiter;
-  h->task = oi::cg_minimize(&h->mail, v, o);
-  return h;
-}
-
-int oi_cg_step(oi_cg* h, double* x_req) {
-  if (!h) return fail(OI_E_ARG, "null handle");
-  if (!h->started) {
-    h->started = true;
-    h->task.start();
-  }
-  if (h->task.done()) return 0;
-  if (!h->mail.pending) return fail(OI_E_ARG, "oi_cg_step: optimiser in an invalid state");
-  if (x_req)
-    for (int k = 0; k < oi::NH; ++k) x_req[k] = h->mail.x[k];
-  return 1;
-}
-
-int oi_cg_feed(oi_cg* h, double f, const double* g) {
-  if (!h || !g) return fail(OI_E_ARG, "null argument");
-  if (!h->mail.pending) return fail(OI_E_ARG, "oi_cg_feed: no pending request");
-  h->mail.f = f;
-  for (int k = 0; k < oi::NH; ++k) h->mail.g[k] = g[k];
-  h->mail.pending = false;
-  h->mail.waiter.resume();
-  return 0;
-}
-
-int oi_cg_result(oi_cg* h, double* x, double* fun, int32_t* nit, int32_t* status, int64_t* nfev,
-                 int64_t* njev, int64_t* nobj) {
-  if (!h || !h->task.done()) return fail(OI_E_ARG, "optimiser not finished");
-  const oi::CgResult& r = h->task.result();
-  if (x)
-    for (int k = 0; k < oi::NH; ++k) x[k] = r.x[k];
-  if (fun) *fun = r.fun;
-  if (nit) *nit = r.nit;
-  if (status) *status = r.status;
-  if (nfev) *nfev = r.nfev;
-  if (njev) *njev = r.njev;
-  if (nobj) *nobj = r.nobj;
-  return 0;
-}
-
-void oi_cg_destroy(oi_cg* h) { delete h; }
 
 const char* oi_last_error(void) { return g_last_error.c_str(); }
 // internal: lets the other translation units (oi_day.cpp) report errors

@@ -68,12 +68,32 @@ def _neighbours(indices):
     return xyt, z[cat], offs, xs
 
 
+_lookup_cache = {'key': None, 'first': None}
+
+
+def _first_match_rows():
+    """GPR:170 ``np.where((X[:,0]==X[index,0]) & (X[:,1]==X[index,1]))`` then
+    ``[0]`` (GPR:171): for every cell the FIRST row of ``X`` with the same
+    coordinates.  Built once per content of ``X`` (keyed on its bytes) instead
+    of once per call, so the reference-style per-cell loop stays O(ncell)."""
+    Xa = np.ascontiguousarray(X, dtype=np.float64)
+    key = (Xa.shape, hash(Xa.tobytes()))
+    if _lookup_cache['key'] != key:
+        # rows sorted by (x, y) with ties by index: a group's first row is its first match
+        order = np.lexsort((np.arange(len(Xa)), Xa[:, 1], Xa[:, 0]))
+        xs, ys = Xa[order, 0], Xa[order, 1]
+        new = np.ones(len(order), dtype=bool)
+        new[1:] = (xs[1:] != xs[:-1]) | (ys[1:] != ys[:-1])
+        grp = np.cumsum(new) - 1
+        first = np.empty(len(Xa), dtype=np.int64)
+        first[order] = order[new][grp]
+        _lookup_cache.update(key=key, first=first)
+    return _lookup_cache['first']
+
+
 def _smoothed_hypers(indices):
     """GPR:170-172: hyper lookup by exact coordinate match (first match)."""
-    first = {}
-    for k in range(len(X) - 1, -1, -1):
-        first[(X[k, 0], X[k, 1])] = k
-    rows = np.array([first[(X[i, 0], X[i, 1])] for i in indices], dtype=np.int64)
+    rows = _first_match_rows()[np.asarray(indices, dtype=np.int64)]
     return np.column_stack([ellXs[rows, 0], ellXs[rows, 1], ellXs[rows, 2], sf2xs[rows], sn2xs[rows]])
 
 
