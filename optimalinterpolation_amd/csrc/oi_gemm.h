@@ -67,12 +67,17 @@ struct StageRegs3 {
   dv2 a, b0, b1;
 };
 
-template <class PairFn>
-__device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
+// MASKED: `skip` (wave-uniform, bit 2*mb + nb) drops this wave's 16x16
+// accumulator blocks that cover only padding rows / columns of a cell (their
+// exact result is 0, which the accumulator already holds).
+template <bool MASKED = false, class PairFn>
+__device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs, PairFn pair,
+                                             unsigned skip = 0u) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = (w >> 2) & 1, wc = w & 3;
   const int nch = npairs * (GNB / KC);  // even
   if (nch == 0) return;
+  if (MASKED) skip = __builtin_amdgcn_readfirstlane(skip);
   const int sk = t >> 5, sm = (t & 31) * 2;  // this thread's 16 B of a 16 x 64 chunk
   const int fr = lane & 15, fk = lane >> 4;
   StageRegs3 r0, r1;
@@ -101,10 +106,10 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
       const double a1 = As[k * LDSA + 32 * wr + 16 + fr];
       const double b0 = Bs[k * LDSB + 32 * wc + fr];
       const double b1 = Bs[k * LDSB + 32 * wc + 16 + fr];
-      acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
-      acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
-      acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
-      acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+      if (!MASKED || !(skip & 1u)) acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+      if (!MASKED || !(skip & 2u)) acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+      if (!MASKED || !(skip & 4u)) acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+      if (!MASKED || !(skip & 8u)) acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
     }
   };
   load(0, r0);
@@ -143,31 +148,41 @@ __device__ __forceinline__ int acc1_col(int nb) {
 // ch is multiplied out of LDS): 66 TF/s vs 57 TF/s for a one-deep prefetch
 // when one operand is L2-resident (tools/gemm_probe3.hip).  Native vector
 // types (not HIP's double2 struct) keep the ring in VGPRs.
-template <class PairFn>
-__device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs, PairFn pair) {
+//
+// `nch` counts 16-deep k-chunks (4 per operand pair; a caller may cut the
+// last pair short when its k rows run into a cell's padding, which holds
+// exact zeros there).  Each thread stages pieces p = t and p = t + 256 of a
+// 16 x 64 chunk (16 B each, row p >> 5): consecutive lanes write consecutive
+// 16 B, so the ds_write_b128 lane groups hit distinct banks.
+// MASKED: `skip` (wave-uniform, bit 2*mb + nb) drops this wave's 16x16
+// accumulator blocks whose outputs are never used (the upper triangle of a
+// diagonal tile, padding rows / columns); their accumulators stay 0.
+template <bool MASKED = false, class PairFn>
+__device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int nch, unsigned skip,
+                                             PairFn pair) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = w >> 1, wc = w & 1;
-  const int nch = npairs * (GNB / KC);  // even
-  if (nch == 0) return;
-  const int sk = t >> 4, sm = (t & 15) * 4;
+  if (nch <= 0) return;
+  const int sk = t >> 5, sm = (t & 31) * 2;
   const int fr = lane & 15, fk = lane >> 4;
+  if (MASKED) skip = __builtin_amdgcn_readfirstlane(skip);
   StageRegs r0, r1;
   auto load = [&](int ch, StageRegs& q) __attribute__((always_inline)) {
     const double *pa, *pb;
     [[clang::always_inline]] pair(ch >> 2, pa, pb);
-    const int off = (ch & 3) * KC * GNB + t * 4;
+    const int off = (ch & 3) * KC * GNB + t * 2;
     q.a0 = gload2(pa + off);
-    q.a1 = gload2(pa + off + 2);
+    q.a1 = gload2(pa + off + 512);
     q.b0 = gload2(pb + off);
-    q.b1 = gload2(pb + off + 2);
+    q.b1 = gload2(pb + off + 512);
   };
   auto store = [&](int buf, const StageRegs& q) __attribute__((always_inline)) {
     double* As = lds + buf * 2 * STAGE_A;
     double* Bs = As + STAGE_A;
     *(dv2*)(As + sk * LDSA + sm) = q.a0;
-    *(dv2*)(As + sk * LDSA + sm + 2) = q.a1;
+    *(dv2*)(As + (sk + 8) * LDSA + sm) = q.a1;
     *(dv2*)(Bs + sk * LDSA + sm) = q.b0;
-    *(dv2*)(Bs + sk * LDSA + sm + 2) = q.b1;
+    *(dv2*)(Bs + (sk + 8) * LDSA + sm) = q.b1;
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
     const double* As = lds + buf * 2 * STAGE_A;
@@ -179,24 +194,25 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int npairs,
       const double a1 = As[k * LDSA + 32 * wr + 16 + fr];
       const double b0 = Bs[k * LDSA + 32 * wc + fr];
       const double b1 = Bs[k * LDSA + 32 * wc + 16 + fr];
-      acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
-      acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
-      acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
-      acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+      if (!MASKED || !(skip & 1u)) acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+      if (!MASKED || !(skip & 2u)) acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+      if (!MASKED || !(skip & 4u)) acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+      if (!MASKED || !(skip & 8u)) acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
     }
   };
   load(0, r0);
-  load(1, r1);
+  load(min(1, nch - 1), r1);
   store(0, r0);
   __syncthreads();
-  // unconditional prefetches: see gemm2_kmajor
+  // unconditional prefetches: see gemm2_kmajor; an odd last chunk skips the
+  // second half-step (the re-loaded duplicate is staged but never used)
   for (int ch = 0; ch < nch; ch += 2) {
     load(min(ch + 2, nch - 1), r0);
     compute(0);
     store(1, r1);
     __syncthreads();
     load(min(ch + 3, nch - 1), r1);
-    compute(1);
+    if (ch + 1 < nch) compute(1);
     if (ch + 2 < nch) store(0, r0);
     __syncthreads();
   }

@@ -34,7 +34,7 @@
 #include "oi_gemm.h"
 
 // GEMM1(acc, lds, npairs, pair): the 64x64 tile-GEMM loop of the panel / lauum kernels
-#define GEMM1(acc, lds, np, ...) gemm1_kmajor(acc, lds, np, __VA_ARGS__)
+#define GEMM1(acc, lds, np, ...) gemm1_kmajor<false>(acc, lds, 4 * (np), 0u, __VA_ARGS__)
 
 #define NB OI_NB
 #define SQRT3 1.7320508075688772
@@ -383,6 +383,17 @@ __global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
   }
 }
 
+// Padding masks: bit 2*mb + nb of a wave's 16x16 accumulator blocks whose
+// rows (m0 = row offset of the wave's quadrant, 16-row blocks mb) or columns
+// (n0, blocks nb) lie at or beyond `mlim` / `nlim` (64 = no padding).
+__device__ __forceinline__ unsigned pad_skip(int m0, int n0, int mlim, int nlim) {
+  unsigned s = 0;
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb)
+      if (m0 + 16 * mb >= mlim || n0 + 16 * nb >= nlim) s |= 1u << (2 * mb + nb);
+  return s;
+}
+
 // --------------------------------------------------- k_chol_panel(j)
 // One 256-thread workgroup per output tile; logical slots of a cell:
 //   x <  T-1-j : tile (i = j+1+x, j) of the factor, one GEMM loop:
@@ -406,13 +417,20 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   const double* Dj = tileD(c, j);
   Quad acc;
   quad_zero(acc);
+  // padding rows of the last block (exact zeros) are skipped per 16x16 block
+  const int rT = c.n - NB * (T - 1);
+  const int wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
   if (x < ntrsm) {
     const int i = j + 1 + x;
-    GEMM1(acc, lds, j + 1 - kbeg, [=, &c](int p, const double*& a, const double*& b) {
+    auto fpair = [=, &c](int p, const double*& a, const double*& b) {
       const int k = kbeg + p;
       a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
       b = tileL(c, i, k);  // k == j: A_ij, already holding A_ij - sum_{k<kbeg} L_ik L_jk^T
-    });
+    };
+    if (i == T - 1 && rT < NB)  // n = row of block row i
+      gemm1_kmajor<true>(acc, lds, 4 * (j + 1 - kbeg), pad_skip(32 * wr, 32 * wc, NB, rT), fpair);
+    else
+      gemm1_kmajor<false>(acc, lds, 4 * (j + 1 - kbeg), 0u, fpair);
     double* Y = tileL(c, i, j);
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
@@ -463,11 +481,15 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   // kbeg > jj: W_j,jj holds Vneg = -sum_{k=jj}^{kbeg-1} L_jk W_k,jj (k_panel_even), so
   // W_j,jj = sum_{k=kbeg}^{j-1} P_jk W_k,jj + Dinv_jj Vneg
   const int kfirst = jj > kbeg ? jj : kbeg, extra = kbeg > jj ? 1 : 0;
-  GEMM1(acc, lds, j - kfirst + extra, [=, &c](int p, const double*& a, const double*& b) {
+  auto wpair = [=, &c](int p, const double*& a, const double*& b) {
     const int k = kfirst + p;
     a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
     b = tileW(c, k, jj);  // k == j: Vneg
-  });
+  };
+  if (j == T - 1 && rT < NB)  // m = row of W block row j
+    gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst + extra), pad_skip(32 * wr, 32 * wc, rT, NB), wpair);
+  else
+    gemm1_kmajor<false>(acc, lds, 4 * (j - kfirst + extra), 0u, wpair);
   double* Wt = tileW(c, j, jj);
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
@@ -534,20 +556,29 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   const double* Dj = tileD(c, j);
   Quad acc;
   quad_zero(acc);
+  // rows / columns of the last block beyond n are padding: their products are
+  // exact zeros (identity padding), so those accumulator blocks are skipped
+  const int rT = c.n - NB * (T - 1);
+  const int w = threadIdx.x >> 6, wr = (w >> 2) & 1, wc = w & 3;
   if (x < ntrsm) {
     const int i = j + 1 + x;
-    gemm2_kmajor(acc, lds, j + 1,
-                 [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
-                   if (p < j) {
-                     a = tileL(c, i, p);
-                     b0 = Pj + (size_t)p * OI_TILE;
-                     b1 = tileL(c, j + 1, p);
-                   } else {
-                     a = tileL(c, i, j);  // A_ij
-                     b0 = Dj;
-                     b1 = g_zero_tile;
-                   }
-                 });
+    auto fpair = [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
+      if (p < j) {
+        a = tileL(c, i, p);
+        b0 = Pj + (size_t)p * OI_TILE;
+        b1 = tileL(c, j + 1, p);
+      } else {
+        a = tileL(c, i, j);  // A_ij
+        b0 = Dj;
+        b1 = g_zero_tile;
+      }
+    };
+    // m = row of block row i; half 1's n = column of block column j+1
+    const int mlim = i == T - 1 ? rT : NB, nlim = (wc >= 2 && j + 1 == T - 1) ? rT : NB;
+    if (mlim < NB || nlim < NB)
+      gemm2_kmajor<true>(acc, lds, j + 1, fpair, pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim));
+    else
+      gemm2_kmajor<false>(acc, lds, j + 1, fpair);
     emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij
     if (x != 0) {
       emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1
@@ -578,12 +609,18 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   }
   const int jj = x - ntrsm;
   if (c.mode != OI_MODE_EVAL || jj >= j) return;
-  gemm2_kmajor(acc, lds, j - jj, [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
+  auto wpair = [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
     const int k = jj + p;
     a = tileW(c, k, jj);
     b0 = Pj + (size_t)k * OI_TILE;
     b1 = has_next ? tileL(c, j + 1, k) : g_zero_tile;
-  });
+  };
+  // n = row of W block row j (half 0) or j+1 (half 1)
+  const int nlim = ((wc < 2 && j == T - 1) || (wc >= 2 && j + 1 == T - 1)) ? rT : NB;
+  if (nlim < NB)
+    gemm2_kmajor<true>(acc, lds, j - jj, wpair, pad_skip(0, 32 * (wc & 1), NB, nlim));
+  else
+    gemm2_kmajor<false>(acc, lds, j - jj, wpair);
   emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);           // W_j,jj (row-major)
   if (has_next) emit_half(acc, 1, lds, tileW(c, j + 1, jj), EMIT_NEG);  // Vneg
 }
@@ -677,15 +714,35 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
   if (*c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
   Quad acc;
   quad_zero(acc);
-  GEMM1(acc, lds, T - i, [=, &c](int p, const double*& a, const double*& b) {
+  // k rows of the last tile beyond n are padding (exact zeros of W off the
+  // padded identity): the last pair's chunks stop at the cell's last row
+  const int n = c.n, rT = n - NB * (T - 1);
+  const int nch = 4 * (T - i - 1) + (rT + KC - 1) / KC;
+  // 16x16 accumulator blocks this wave may drop: the upper triangle of a
+  // diagonal tile (never read below) and padding rows / columns
+  const int w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  unsigned skip = 0;
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb) {
+      const int m0 = 32 * wr + 16 * mb, n0 = 32 * wc + 16 * nb;
+      const bool upper = i == j && m0 + 15 < n0;
+      const bool pad = (i == T - 1 && m0 >= rT) || (j == T - 1 && n0 >= rT);
+      if (upper || pad) skip |= 1u << (2 * mb + nb);
+    }
+  auto wpair = [=, &c](int p, const double*& a, const double*& b) {
     a = tileW(c, i + p, i);
     b = tileW(c, i + p, j);
-  });
+  };
+  if (i == j || i == T - 1)
+    gemm1_kmajor<true>(acc, lds, nch, skip, wpair);
+  else
+    gemm1_kmajor<false>(acc, lds, nch, 0u, wpair);
   double* uQ = lds;            // [3][128]: rows 0..63, columns 64..127
   double* uq = lds + 3 * 128;  // [3][128]
   double* al = lds + 6 * 128;  // [128]
   double* red = lds + 7 * 128;
-  const int t = threadIdx.x, n = c.n;
+  const int t = threadIdx.x;
+  __syncthreads();  // the GEMM's last LDS reads are done before the epilogue reuses lds
   if (t < 128) {
     const int a = t < 64 ? i * NB + t : j * NB + (t - 64);
     for (int d = 0; d < 3; ++d) {
