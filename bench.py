@@ -546,9 +546,18 @@ def heartbeat(period=60.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
-def roofline_of(prof, evals, n, dt):
+def site_counts(cells):
+    """Distinct (x, y, t) sites per cell: the size of the problem the library
+    solves (oi_device.h "Duplicate sites"); host-side, for the flop model."""
+    v = np.ascontiguousarray(cells.xyt).view(np.dtype((np.void, 24))).ravel()
+    return np.array([len(np.unique(v[a:b])) for a, b in zip(cells.offs[:-1], cells.offs[1:])], dtype=np.int64)
+
+
+def roofline_of(prof, evals, n, dt, n_obs=None):
     """Roofline of the dominant kernel from the library's HIP-event profile
-    (every launch of the timed region, on the stream the kernels run on)."""
+    (every launch of the timed region, on the stream the kernels run on).
+    ``n``: the solved size per cell (distinct sites); ``n_obs``: observations
+    (the reference's n x n problem) for the reference-equivalent rate."""
     kern = prof['kernels']
     gemm = {k: v for k, v in kern.items() if v['flops'] > 0 and v['total_ms'] > 0}
     dom = max(gemm, key=lambda k: gemm[k]['total_ms']) if gemm else max(kern, key=lambda k: kern[k]['total_ms'])
@@ -575,15 +584,18 @@ def roofline_of(prof, evals, n, dt):
         except Exception:
             traffic = None
     useful = float(np.sum(evals * (n ** 3 + 40 * n ** 2) + n ** 3 / 3 + 16 * n ** 2))
+    no = n if n_obs is None else n_obs
+    ref_eq = float(np.sum(evals * (no ** 3 + 40 * no ** 2) + no ** 3 / 3 + 16 * no ** 2))
     return {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
             "traffic_note": ("HBM bytes per launch of this kernel, rocprofv3 PMC FETCH_SIZE(x2, gfx950)+WRITE_SIZE, "
                              "profiles/pmc_traffic.json") if traffic is not None else None,
             "launches": kd['launches'], "avg_launch_ms": kd['total_ms'] / max(kd['launches'], 1),
             "flops_per_launch": alg_dom / max(kd['launches'], 1),
-            "flop_model": ("algorithmic: SURVEY §8d potrf+trtri 2n^3/3 per eval (+ potrf n^3/3 per predict) "
-                           "for the factor kernels, lauum n^3/3 per eval for k_lauum_grad, unpadded n, "
-                           "split over a family's kernels by executed tile products"),
+            "flop_model": ("algorithmic: SURVEY §8d potrf+trtri 2m^3/3 per eval (+ potrf m^3/3 per predict) "
+                           "for the factor kernels, lauum m^3/3 per eval for k_lauum_grad, m = the cell's "
+                           "distinct sites (the m x m problem solved, oi_device.h), unpadded, split over a "
+                           "family's kernels by executed tile products"),
             "achieved_executed": round(achieved_exec, 3),
             "frac_executed": round(achieved_exec / PEAK_FP64_TFLOPS, 4),
             "executed_flops_per_launch": kd['flops'] / max(kd['launches'], 1),
@@ -591,7 +603,11 @@ def roofline_of(prof, evals, n, dt):
             "kernels_ms": {k: round(v['total_ms'], 3) for k, v in kern.items() if v['launches']},
             "useful_tflops_per_gpu": round(useful / dt / 1e12, 3),
             "useful_frac_per_gpu": round(useful / dt / 1e12 / PEAK_FP64_TFLOPS, 4),
-            "useful_flop_model": "SURVEY §8d: E*(n^3+40n^2) + n^3/3 + 16n^2 per cell, unpadded n"}
+            "useful_flop_model": "SURVEY §8d: E*(m^3+40m^2) + m^3/3 + 16m^2 per cell, m distinct sites",
+            "reference_equivalent_tflops_per_gpu": round(ref_eq / dt / 1e12, 3),
+            "reference_equivalent_model": ("the same formula on n observations: the n x n work the reference's "
+                                           "algorithm does per cell, / the measured time"),
+            "sites_over_obs_mean": round(float(np.mean(n / np.maximum(no, 1))), 4)}
 
 
 def main():
@@ -707,8 +723,9 @@ def main():
     info = np.concatenate([outs[k][2] for k in range(done_k)])
     status = np.concatenate([outs[k][1] for k in range(done_k)])
     sizes_timed = np.concatenate([np.diff(slices[k].offs) for k in range(done_k)])
+    sites_timed = np.concatenate([site_counts(slices[k]) for k in range(done_k)])
     evals = info[:, 3].astype(float) if opt else np.zeros(len(sizes_timed))
-    n = sizes_timed.astype(float)
+    n = sites_timed.astype(float)
     line = {"metric": METRIC if args.workload in ('day', 'days') else f"grid-cells/sec ({args.workload}), fp64",
             "value": round(total_cells / dt, 4), "unit": "grid-cells/s", "n_gpus": world,
             "steps": done_k, "warmup": args.warmup, "ms_per_step": round(dt / max(done_k, 1) * 1e3, 3),
@@ -716,7 +733,7 @@ def main():
             "data": "synthetic (seeded SURVEY §8d generator; reference data not shipped)",
             "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
             "failed_cells": int(np.sum(status != 0)), "timed_s": round(dt, 3),
-            "roofline": roofline_of(prof, evals, n, dt)}
+            "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float))}
     if done_k != args.steps or truncated:
         line.update({"truncated": True, "steps_requested": args.steps})
     if rank == 0:

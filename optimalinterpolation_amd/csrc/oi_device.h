@@ -22,6 +22,24 @@ enum OiMode { OI_MODE_EVAL = 0, OI_MODE_PREDICT = 1 };
 // per-cell status bits (device-written)
 enum OiStatus { OI_OK = 0, OI_NOT_PD = 1 };
 
+// Duplicate sites.  Observations with identical (x, y, t) (several
+// satellites binned into one grid cell on one day) give identical rows of K.
+// With n observations at m distinct sites, incidence P (n x m), counts
+// c = diag(P^T P), d = sqrt(c) and Kd the m x m kernel of the sites,
+//   K + sn2 I = sn2 I + P Kd P^T,   M = D Kd D + sn2 I  (m x m, D = diag d)
+// and exactly (no approximation):
+//   log det(K + sn2 I) = (n - m) log sn2 + log det M
+//   r^T (K + sn2 I)^-1 r = SSW / sn2 + v^T M^-1 v,   v = D^-1 P^T r,
+//                          SSW = sum_a (r_a - mean of r over a's site)^2
+//   P^T (K + sn2 I)^-1 P = D M^-1 D,   P^T alpha = u = D M^-1 v
+//   tr((K + sn2 I)^-1) - alpha^T alpha = (n - m)/sn2 - SSW/sn2^2
+//                                        + tr(M^-1) - |M^-1 v|^2
+// so SMLII's nlZ and gradient (GPR:124-138) and the predict block
+// (GPR:173-182, k* = P kd*) follow from an m x m problem: the kernels below
+// run on the SITES (n = m, xyt = site coordinates, r = v, dw = d) and the
+// (n - m), SSW terms are added at the end.  Without duplicates m = n, d = 1,
+// v = r, SSW = 0 and every formula is the plain one.  k_dedup (once per cell,
+// at submission) builds the sites.
 struct OiCell {
   double* L;          // packed lower tiles (T(T+1)/2 * 4096)
   double* W;          // packed lower tiles of L^-1 (eval mode), else null
@@ -29,15 +47,17 @@ struct OiCell {
   double* P;          // T * 4096: P_jk = -Dinv_jj L_jk of the current block column
   double* vec;        // 4 * T * 64: z | alpha | kstar | v
   double* part;       // partial sums, see OI_PART_*
-  const double* xyt;  // n x 3 inputs (device)
-  const double* r;    // n residuals y - mX (device)
+  const double* xyt;  // n x 3 site coordinates (device)
+  const double* r;    // n site residuals v = D^-1 P^T (y - mX) (device)
+  const double* dw;   // n site weights d = sqrt(count) (device)
   double* out;        // OI_OUT_N doubles of results
   int32_t* status;    // one int
-  int32_t n, T, mode, pad_;
+  int32_t n, T, mode, n_obs;  // n = sites m; n_obs = observations
   double hyp[5];      // lx, ly, lt, sf2, sn2 (the values the objective uses)
   double xs[3];       // prediction target (predict mode)
   double mean;        // prior mean (predict mode)
-  double pad2_[2];
+  double ssw;         // within-site residual sum of squares SSW
+  double pad2_;
 };
 
 // partial-sum layout inside OiCell::part (ntile = T(T+1)/2)
@@ -72,6 +92,14 @@ int oi_launch_predict(const OiCell* cells, const int32_t* list, int ncell, void*
 int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, void* stream);
 // r[a] = y[a] - (mX ? mX[a] : 1.0 * mean)
 int oi_set_debug(int on);
+// Sites of every cell of a batch (one workgroup per cell): offs (device,
+// ncell+1) index xyt / r by observation; outputs at the same offsets: site
+// coordinates (3 per site), v, d; per cell m and SSW.  nodup: every
+// observation its own site (m = n, d = 1, v = r, SSW = 0).  maxn: the largest
+// n of the batch (sizes the LDS).
+int oi_launch_dedup(const double* xyt, const double* r, const int64_t* offs, int ncell, int maxn,
+                    int nodup, double* sites, double* v, double* dw, int32_t* mcount, double* ssw,
+                    void* stream);
 int oi_launch_residual(const double* y, const double* mX, double mean, double* r, int64_t N,
                        void* stream);
 #ifdef __cplusplus

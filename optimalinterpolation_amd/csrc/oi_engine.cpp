@@ -279,13 +279,24 @@ struct Job {
   int32_t* info = nullptr;
   double* nlz = nullptr;        // EVAL_ONLY
   double* grad = nullptr;
+  // distinct sites per cell (k_dedup; oi_device.h "Duplicate sites")
+  const double* sites = nullptr;  // device, 3 per site at the cell's observation offset
+  const double* v = nullptr;      // device, site residuals
+  const double* dw = nullptr;     // device, site weights
+  std::vector<int32_t> m;         // sites per cell
+  std::vector<double> ssw;        // within-site residual sum of squares per cell
   // bookkeeping
   int64_t id = 0;
   int64_t remaining = 0;
-  size_t in_off = SIZE_MAX, in_bytes = 0;  // arena block holding xyt copy + r
+  size_t in_off = SIZE_MAX, in_bytes = 0;  // arena block holding the inputs' device copies
   DBuf own;                                // fallback when the arena is full
   std::vector<double> r_host;              // staging for host inputs
 };
+
+bool dedup_enabled() {
+  const char* e = getenv("OI_DEDUP");
+  return !(e && atoi(e) == 0);
+}
 
 struct Slot {
   Job* job = nullptr;
@@ -377,23 +388,20 @@ class Engine {
   int64_t submit(std::unique_ptr<Job> job, const double* xyt_in, const double* y, const double* mX) {
     Job& jb = *job;
     jb.id = next_id_++;
-    const int64_t N = jb.offs[jb.ncell];
-    size_t max_cell = 0;
-    for (int64_t c = 0; c < jb.ncell; ++c)
-      max_cell = std::max(max_cell, cell_bytes(jb.offs[c + 1] - jb.offs[c], jb.kind != Job::PREDICT_ONLY));
-    if (max_cell > ctx_.arena.size())
-      throw NoMem("a cell needs " + std::to_string(max_cell) + " bytes of workspace, pool is " +
-                  std::to_string(ctx_.arena.size()));
+    const int64_t N = jb.offs[jb.ncell], nc = jb.ncell;
     // device inputs: order after the caller's stream (or the legacy null
     // stream, torch's default) so producers of xyt / y / mX have finished
     if (o_.device_inputs && N > 0) {
       HIPC(hipEventRecord(ready_, o_.stream ? (hipStream_t)o_.stream : (hipStream_t)0));
       for (Group& gr : groups_) HIPC(hipStreamWaitEvent(gr.st, ready_, 0));
     }
-    // workspace for the residuals (and the host inputs' device copy)
-    const size_t rb = (size_t)std::max<int64_t>(N, 1) * 8;
-    const size_t xb = o_.device_inputs ? 0 : (size_t)std::max<int64_t>(N, 1) * 24;
-    jb.in_bytes = ((rb + 255) & ~size_t(255)) + xb;
+    // one block: residuals | sites | v | d | offs | m | SSW (| host inputs' copy)
+    auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t N1 = (size_t)std::max<int64_t>(N, 1), C1 = (size_t)std::max<int64_t>(nc, 1);
+    const size_t sz[8] = {rnd(N1 * 8), rnd(N1 * 24), rnd(N1 * 8), rnd(N1 * 8), rnd((C1 + 1) * 8),
+                          rnd(C1 * 4), rnd(C1 * 8), o_.device_inputs ? 0 : rnd(N1 * 24)};
+    jb.in_bytes = 0;
+    for (size_t b : sz) jb.in_bytes += b;
     jb.in_off = ctx_.arena.alloc(jb.in_bytes);
     char* base;
     if (jb.in_off != SIZE_MAX) {
@@ -402,39 +410,75 @@ class Engine {
       jb.own.reserve(jb.in_bytes);
       base = (char*)jb.own.p;
     }
-    double* d_r = (double*)base;
-    jb.r = d_r;
+    char* q = base;
+    auto take = [&](size_t b) {
+      char* p = q;
+      q += b;
+      return p;
+    };
+    double* d_r = (double*)take(sz[0]);
+    double* d_sites = (double*)take(sz[1]);
+    double* d_v = (double*)take(sz[2]);
+    double* d_dw = (double*)take(sz[3]);
+    int64_t* d_offs = (int64_t*)take(sz[4]);
+    int32_t* d_m = (int32_t*)take(sz[5]);
+    double* d_ssw = (double*)take(sz[6]);
+    const double* d_x = xyt_in;
     if (o_.device_inputs) {
-      jb.xyt = xyt_in;
       if (N > 0 && oi_launch_residual(y, mX, jb.mean, d_r, N, st_))
         throw HipError("residual kernel launch failed");
     } else {
-      double* d_x = (double*)(base + ((rb + 255) & ~size_t(255)));
-      jb.xyt = d_x;
+      double* dx = (double*)take(sz[7]);
+      d_x = dx;
       if (N > 0) {
         jb.r_host.resize(N);
         for (int64_t a = 0; a < N; ++a) jb.r_host[a] = y[a] - (mX ? mX[a] : 1.0 * jb.mean);
-        HIPC(hipMemcpyAsync(d_x, xyt_in, N * 3 * 8, hipMemcpyHostToDevice, st_));
+        HIPC(hipMemcpyAsync(dx, xyt_in, N * 3 * 8, hipMemcpyHostToDevice, st_));
         HIPC(hipMemcpyAsync(d_r, jb.r_host.data(), N * 8, hipMemcpyHostToDevice, st_));
-        HIPC(hipStreamSynchronize(st_));  // host inputs may be released on return
       }
+    }
+    // distinct sites of every cell; the host needs m to size and order cells
+    jb.m.assign(nc, 0);
+    jb.ssw.assign(nc, 0.0);
+    if (nc > 0) {
+      int64_t maxn = 0;
+      for (int64_t c = 0; c < nc; ++c) maxn = std::max(maxn, jb.offs[c + 1] - jb.offs[c]);
+      HIPC(hipMemcpyAsync(d_offs, jb.offs.data(), (nc + 1) * 8, hipMemcpyHostToDevice, st_));
+      if (oi_launch_dedup(d_x, d_r, d_offs, (int)nc, (int)std::min<int64_t>(maxn, INT32_MAX),
+                          dedup_enabled() ? 0 : 1, d_sites, d_v, d_dw, d_m, d_ssw, st_))
+        throw HipError(std::string("dedup kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+      HIPC(hipMemcpyAsync(jb.m.data(), d_m, nc * 4, hipMemcpyDeviceToHost, st_));
+      HIPC(hipMemcpyAsync(jb.ssw.data(), d_ssw, nc * 8, hipMemcpyDeviceToHost, st_));
+    }
+    HIPC(hipStreamSynchronize(st_));  // m known; host inputs may be released on return
+    jb.xyt = d_x;
+    jb.r = d_r;
+    jb.sites = d_sites;
+    jb.v = d_v;
+    jb.dw = d_dw;
+    size_t max_cell = 0;
+    for (int64_t c = 0; c < nc; ++c)
+      max_cell = std::max(max_cell, cell_bytes(jb.m[c], jb.kind != Job::PREDICT_ONLY));
+    if (max_cell > ctx_.arena.size()) {
+      ctx_.arena.release(jb.in_off, jb.in_bytes);
+      jb.in_off = SIZE_MAX;
+      throw NoMem("a cell needs " + std::to_string(max_cell) + " bytes of workspace, pool is " +
+                  std::to_string(ctx_.arena.size()));
     }
     if (G_ > 1) {  // the other groups' streams see the inputs
       HIPC(hipEventRecord(ready_, st_));
       for (Group& gr : groups_)
         if (gr.st != st_) HIPC(hipStreamWaitEvent(gr.st, ready_, 0));
     }
-    // admission order inside the batch: largest cells first (cost ~ n^3), ties by index
-    std::vector<int64_t> order(jb.ncell);
+    // admission order inside the batch: largest cells first (cost ~ m^3), ties by index
+    std::vector<int64_t> order(nc);
     std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-      return jb.offs[a + 1] - jb.offs[a] > jb.offs[b + 1] - jb.offs[b];
-    });
-    jb.remaining = jb.ncell;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return jb.m[a] > jb.m[b]; });
+    jb.remaining = nc;
     Job* jp = job.get();
     const int64_t id = jb.id;
     for (int64_t c : order) queue_.push_back({jp, c});
-    if (jb.ncell == 0)
+    if (nc == 0)
       release_job(jp);
     else
       jobs_[id] = std::move(job);
@@ -500,7 +544,7 @@ class Engine {
       Job* jp = queue_.front().first;
       const int64_t c = queue_.front().second;
       const Job& job = *jp;
-      const int64_t n = job.offs[c + 1] - job.offs[c];
+      const int64_t n = job.m[c];  // the cell's problem size: its distinct sites
       const bool eval_mem = job.kind != Job::PREDICT_ONLY;
       const size_t bytes = cell_bytes(n, eval_mem);
       const size_t off = ctx_.arena.alloc(bytes);
@@ -532,11 +576,14 @@ class Engine {
       cd.P = take((size_t)T * OI_TILE * 8);
       cd.vec = take(4 * (size_t)T * OI_NB * 8);
       cd.part = take((size_t)OI_PART_SIZE(nt, T) * 8);
-      cd.xyt = job.xyt + 3 * job.offs[c];
-      cd.r = job.r + job.offs[c];
+      cd.xyt = job.sites + 3 * job.offs[c];
+      cd.r = job.v + job.offs[c];
+      cd.dw = job.dw + job.offs[c];
       cd.out = (double*)d_res_.p + (size_t)s * OI_OUT_N;
       cd.status = (int32_t*)d_stat_.p + s;
       cd.n = (int32_t)n;
+      cd.n_obs = (int32_t)(job.offs[c + 1] - job.offs[c]);
+      cd.ssw = job.ssw[c];
       cd.T = T;
       if (!job.xs.empty())
         for (int d = 0; d < 3; ++d) cd.xs[d] = job.xs[3 * c + d];

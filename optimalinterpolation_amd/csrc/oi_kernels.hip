@@ -124,7 +124,8 @@ __device__ __forceinline__ bool xcd_cell_slot_lead0(int gx, int ncell, int& cell
 }
 
 // ------------------------------------------------------------- k_build
-// K + sn2*I for tile (i, j), GPR:93-94 and GPR:126; identity on padding.
+// M = D Kd D + sn2 I for tile (i, j) (K + sn2 I of GPR:93-94 / GPR:126 on the
+// sites, oi_device.h); identity on padding.
 __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
                                                const int32_t* __restrict__ list, int gx,
                                                int ncell) {
@@ -134,10 +135,12 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
   int i, j;
   if (!decode_tri(x, c.T, i, j)) return;
   __shared__ double u[2][3][NB];
+  __shared__ double dws[2][NB];
   const int t = threadIdx.x, n = c.n;
   if (t < 2 * NB) {
     int side = t >> 6, idx = t & 63, a = (side ? j : i) * NB + idx;
     for (int d = 0; d < 3; ++d) u[side][d][idx] = a < n ? (SQRT3 * c.xyt[3 * a + d]) / c.hyp[d] : 0.0;
+    dws[side][idx] = a < n ? c.dw[a] : 0.0;
   }
   __syncthreads();
   const double sf2 = c.hyp[3], sn2 = c.hyp[4];
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
     } else {
       double d0 = u[0][0][r] - u[1][0][cc], d1 = u[0][1][r] - u[1][1][cc], d2 = u[0][2][r] - u[1][2][cc];
       double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-      val = sf2 * ((1.0 + Q) * exp(-Q));
+      val = (dws[0][r] * dws[1][cc]) * (sf2 * ((1.0 + Q) * exp(-Q)));  // M = D Kd D (+ sn2 I)
       if (a == b) val += sn2;
     }
     Y[e] = val;
@@ -740,7 +743,8 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
   double* uQ = lds;            // [3][128]: rows 0..63, columns 64..127
   double* uq = lds + 3 * 128;  // [3][128]
   double* al = lds + 6 * 128;  // [128]
-  double* red = lds + 7 * 128;
+  double* dl = lds + 7 * 128;  // [128] site weights d
+  double* red = lds + 8 * 128;
   const int t = threadIdx.x;
   __syncthreads();  // the GEMM's last LDS reads are done before the epilogue reuses lds
   if (t < 128) {
@@ -751,6 +755,7 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
       uq[d * 128 + t] = SQRT3 * (xv / c.hyp[d]);
     }
     al[t] = c.vec[T * NB + a];
+    dl[t] = a < n ? c.dw[a] : 0.0;
   }
   __syncthreads();
   const double sf2 = c.hyp[3];
@@ -762,7 +767,8 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
         const int a = i * NB + m, b = j * NB + nn;
         if (a >= n || b >= n || (i == j && m < nn)) continue;
         const double wgt = (a == b) ? 1.0 : 2.0;
-        const double w = acc.c[mb][nb][r] - al[m] * al[64 + nn];
+        const double w0 = acc.c[mb][nb][r] - al[m] * al[64 + nn];  // (M^-1 - aa^T)_st
+        const double w = (dl[m] * dl[64 + nn]) * w0;                // (D M^-1 D - uu^T)_st
         const double d0 = uQ[0 * 128 + m] - uQ[0 * 128 + 64 + nn];
         const double d1 = uQ[1 * 128 + m] - uQ[1 * 128 + 64 + nn];
         const double d2 = uQ[2 * 128 + m] - uQ[2 * 128 + 64 + nn];
@@ -776,7 +782,7 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
         s[1] += wgt * (w * (sf2 * ((q1 * q1) * e)));
         s[2] += wgt * (w * (sf2 * ((q2 * q2) * e)));
         s[3] += wgt * (w * (2.0 * K));
-        if (a == b) s[4] += w;
+        if (a == b) s[4] += w0;
       }
   block_sum<5, 4>(s, red);
   if (t == 0) {
@@ -807,13 +813,16 @@ __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cel
   }
   block_sum<7, 4>(v, red);
   if (t == 0) {
-    const double quad = v[5], logdet = v[6];
-    c.out[0] = (quad / 2 + logdet) + (c.n * LOG2PI) / 2;
+    // site form (oi_device.h): r^T alpha = SSW/sn2 + v^T M^-1 v,
+    // sum log diag L = log det M / 2 + (n - m)/2 log sn2, tr Q += (n - m)/sn2 - SSW/sn2^2
+    const double quad = v[5], logdet = v[6], sn2 = c.hyp[4];
+    const double nm = (double)(c.n_obs - c.n);
+    c.out[0] = ((quad + c.ssw / sn2) / 2 + (logdet + (nm / 2) * log(sn2))) + (c.n_obs * LOG2PI) / 2;
     c.out[1] = v[0] / 2;
     c.out[2] = v[1] / 2;
     c.out[3] = v[2] / 2;
     c.out[4] = v[3] / 2;
-    c.out[5] = c.hyp[4] * v[4];
+    c.out[5] = sn2 * ((v[4] + nm / sn2) - c.ssw / (sn2 * sn2));
     c.out[6] = 0.0;
   }
 }
@@ -850,7 +859,7 @@ __global__ __launch_bounds__(256) void k_predict(const OiCell* __restrict__ cell
         double d1 = (SQRT3 * c.xyt[3 * a + 1]) / c.hyp[1] - xs1;
         double d2 = (SQRT3 * c.xyt[3 * a + 2]) / c.hyp[2] - xs2;
         double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-        kv = sf2 * ((1.0 + Q) * exp(-Q));
+        kv = c.dw[a] * (sf2 * ((1.0 + Q) * exp(-Q)));  // D kd* (k* = P kd*)
       }
       ks[a] = kv;
     }
@@ -926,10 +935,146 @@ __global__ __launch_bounds__(256) void k_predict(const OiCell* __restrict__ cell
   }
   block_sum<4, 4>(acc5, red);
   if (t == 0) {
+    const double sn2 = c.hyp[4], nm = (double)(c.n_obs - n);
     c.out[0] = c.mean + acc5[0];
     c.out[1] = sqrt(sf2 - acc5[1]);
-    c.out[2] = ((-acc5[2]) / 2 - acc5[3]) - (n * LOG2PI) / 2;
+    c.out[2] = ((-(acc5[2] + c.ssw / sn2)) / 2 - (acc5[3] + (nm / 2) * log(sn2))) - (c.n_obs * LOG2PI) / 2;
   }
+}
+
+// ------------------------------------------------------------- k_dedup
+// Distinct observation sites of each cell (oi_device.h, "Duplicate sites"),
+// one workgroup per cell, once per submitted batch.  Site s = the s-th first
+// occurrence in observation order; prev[a] = the latest earlier observation
+// with bitwise-equal (x, y, t), nxt the reverse link, so every site's
+// observations are walked in observation order: fixed-order sums, results
+// independent of the batch.  Coordinates are staged in LDS for n <= 4096
+// (36 B per observation with the links), read from global memory above.
+#define DEDUP_LDS_N 4096
+#define DEDUP_MAX_N 13000  // 8 B x 13000 <= 36 B x 4096
+__global__ __launch_bounds__(256) void k_dedup(const double* __restrict__ xyt,
+                                               const double* __restrict__ r,
+                                               const int64_t* __restrict__ offs, int nodup,
+                                               double* __restrict__ sites, double* __restrict__ v,
+                                               double* __restrict__ dw, int32_t* __restrict__ mcount,
+                                               double* __restrict__ ssw) {
+  extern __shared__ double sh[];
+  __shared__ int scan[256];
+  __shared__ double red[4];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int64_t a0 = offs[c];
+  const int n = (int)(offs[c + 1] - a0);
+  const double* X = xyt + 3 * a0;
+  const double* R = r + a0;
+  const bool single = nodup || n > DEDUP_MAX_N;  // every observation its own site
+  const bool in_lds = !single && n <= DEDUP_LDS_N;
+  double* cx = sh;
+  double* cy = sh + n;
+  double* ct = sh + 2 * n;
+  int* prev = (int*)(sh + (in_lds ? 3 * n : 0));
+  int* nxt = prev + n;
+  if (in_lds)
+    for (int b = t; b < n; b += 256) {
+      cx[b] = X[3 * b];
+      cy[b] = X[3 * b + 1];
+      ct[b] = X[3 * b + 2];
+    }
+  if (!single)
+    for (int a = t; a < n; a += 256) nxt[a] = -1;
+  __syncthreads();
+  if (!single) {
+    for (int a = t; a < n; a += 256) {
+      int p = -1;
+      if (in_lds) {
+        const double xa = cx[a], ya = cy[a], ta = ct[a];
+        for (int b = a - 1; b >= 0; --b)
+          if (cx[b] == xa && cy[b] == ya && ct[b] == ta) {
+            p = b;
+            break;
+          }
+      } else {
+        const double xa = X[3 * a], ya = X[3 * a + 1], ta = X[3 * a + 2];
+        for (int b = a - 1; b >= 0; --b)
+          if (X[3 * b] == xa && X[3 * b + 1] == ya && X[3 * b + 2] == ta) {
+            p = b;
+            break;
+          }
+      }
+      prev[a] = p;
+    }
+    __syncthreads();
+    for (int a = t; a < n; a += 256)
+      if (prev[a] >= 0) nxt[prev[a]] = a;
+  }
+  // exclusive scan of first-occurrence flags over contiguous segments
+  const int seg = (n + 255) / 256, s0 = min(n, t * seg), s1 = min(n, s0 + seg);
+  int cnt = 0;
+  for (int a = s0; a < s1; ++a) cnt += (single || prev[a] < 0) ? 1 : 0;
+  scan[t] = cnt;
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int q = 0; q < 256; ++q) {
+      const int x = scan[q];
+      scan[q] = acc;
+      acc += x;
+    }
+    mcount[c] = acc;
+  }
+  __syncthreads();
+  int s = scan[t];
+  double part = 0.0;
+  for (int a = s0; a < s1; ++a) {
+    if (!(single || prev[a] < 0)) continue;
+    double rs = 0.0, cntd = 0.0;
+    if (single) {
+      rs = R[a];
+      cntd = 1.0;
+    } else {
+      for (int b = a; b >= 0; b = nxt[b]) {
+        rs += R[b];
+        cntd += 1.0;
+      }
+      const double rbar = rs / cntd;
+      for (int b = a; b >= 0; b = nxt[b]) {
+        const double e = R[b] - rbar;
+        part += e * e;
+      }
+    }
+    const double d = sqrt(cntd);
+    const int64_t o = a0 + s;
+    sites[3 * o] = X[3 * a];
+    sites[3 * o + 1] = X[3 * a + 1];
+    sites[3 * o + 2] = X[3 * a + 2];
+    v[o] = rs / d;
+    dw[o] = d;
+    ++s;
+  }
+  for (int o = 32; o >= 1; o >>= 1) part += __shfl_down(part, o, 64);
+  if ((t & 63) == 0) red[t >> 6] = part;
+  __syncthreads();
+  if (t == 0) ssw[c] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+extern "C" int oi_launch_dedup(const double* xyt, const double* r, const int64_t* offs, int ncell,
+                               int maxn, int nodup, double* sites, double* v, double* dw,
+                               int32_t* mcount, double* ssw, void* stream) {
+  if (ncell <= 0) return 0;
+  // LDS: coordinates + links (36 B per observation) for n <= DEDUP_LDS_N,
+  // links only (8 B) above; cells beyond DEDUP_MAX_N run without deduplication
+  size_t lds = 0;
+  if (!nodup && maxn > 0)
+    lds = maxn <= DEDUP_LDS_N ? (size_t)36 * maxn
+                              : (size_t)36 * DEDUP_LDS_N;  // >= 8 * DEDUP_MAX_N
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_dedup, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              36 * DEDUP_LDS_N);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_dedup, dim3(ncell), dim3(256), lds, (hipStream_t)stream, xyt, r, offs, nodup,
+                     sites, v, dw, mcount, ssw);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------- k_residual

@@ -209,3 +209,50 @@ def test_config5_size_n5000():
     for got, ref in ((out[0, 0], fs[0]), (out[0, 1], sd[0])):
         ok, err = close(got, ref)
         assert ok, (got, ref, err)
+
+
+def test_duplicate_sites_reduction():
+    """The site form (oi_device.h "Duplicate sites"): observations with equal
+    (x, y, t) are folded into one site of weight sqrt(count) and the (n - m),
+    SSW terms added back -- exact algebra, so nlZ / gradient / predict agree
+    with the oracle's n x n computation (GPR:107-141, 173-182) at T1, with
+    deduplication on (default) and off (OI_DEDUP=0), including a cell beyond
+    the kernel's LDS staging size (n = 4500) and one made only of copies of a
+    single site."""
+    import os
+    rng = np.random.default_rng(8)
+    sizes = [3, 200, 700, 4500]
+    cells = synthetic.make_cells(sizes, seed=31)
+    xyt, z = cells.xyt.copy(), cells.z.copy()
+    a = int(cells.offs[0])
+    xyt[a + 1] = xyt[a]
+    xyt[a + 2] = xyt[a]                      # cell 0: three copies of one site
+    b = int(cells.offs[1])
+    xyt[b:b + 50] = xyt[b + 50:b + 100]      # cell 1: 50 extra duplicates
+    h = np.tile([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(8e-4), 0.0], (4, 1))
+    mX = np.full(len(z), cells.mean)
+    res = {}
+    for mode in ('1', '0'):
+        os.environ['OI_DEDUP'] = mode
+        try:
+            res[mode] = _lib.nlml_grad_batch(xyt, z, mX, cells.offs, h)
+            hyp = np.tile(np.exp(h[0, :5]), (4, 1))
+            res[mode + 'p'] = _lib.gpr_batch(xyt, z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+        finally:
+            os.environ.pop('OI_DEDUP', None)
+    for c in range(4):
+        lo, hi = int(cells.offs[c]), int(cells.offs[c + 1])
+        x, y = xyt[lo:hi], z[lo:hi]
+        f, g = O.neg_log_ml(h[c], x, y, np.ones(len(y)) * cells.mean)
+        f = float(np.asarray(f).item())
+        S = grad_scale(h[c], x, y, np.ones(len(y)) * cells.mean) if len(y) <= 1000 else np.abs(g) + 1e-6 * np.abs(f)
+        fs, sd, lZ = O.predict(x, y, cells.xs[c:c + 1], cells.mean, np.exp(h[c, :3]), np.exp(h[c, 3]),
+                               np.exp(h[c, 4]))
+        for mode in ('1', '0'):
+            nlz, grad, st = res[mode]
+            out = res[mode + 'p'][0]
+            assert st[c] == 0
+            assert close(nlz[c], f)[0], (mode, c, nlz[c], f)
+            assert np.all(np.abs(grad[c, :5] - g[:5]) <= RTOL * (np.abs(g[:5]) + S[:5])), (mode, c, grad[c], g)
+            assert close(out[c, 0], fs[0])[0] and close(out[c, 1], sd[0])[0] and close(out[c, 2], lZ)[0], \
+                (mode, c, out[c, :3], fs, sd, lZ)
