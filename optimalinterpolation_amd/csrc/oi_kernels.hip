@@ -144,6 +144,11 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
   }
   __syncthreads();
   const double sf2 = c.hyp[3], sn2 = c.hyp[4];
+  // Duplicate sites make K + sn2 I singular up to sn2: the reference's
+  // n x n Cholesky loses the pivot of a repeated row, (sf2 + sn2) - sf2^2 /
+  // (sf2 + sn2), once sf2 + sn2 rounds to sf2 (sn2 = 0 included) and takes
+  // the LinAlgError branch (GPR:139-140); the m x m site form would not notice.
+  if (x == 0 && t == 0 && c.n_obs > n && sf2 + sn2 == sf2) *c.status = OI_NOT_PD;
   double* Y = tileL(c, i, j);
   for (int e = t; e < OI_TILE; e += 256) {
     int r = e & 63, cc = e >> 6, a = i * NB + r, b = j * NB + cc;
