@@ -45,7 +45,8 @@ struct OiCell {
   double* W;          // packed lower tiles of L^-1 (eval mode), else null
   double* Dinv;       // T * 4096
   double* P;          // T * 4096: P_jk = -Dinv_jj L_jk of the current block column
-  double* vec;        // 4 * T * 64: z | alpha | kstar | v
+  double* vec;        // 4 * T * 64: z | alpha | kstar | v.  z = L^-1 r and (predict)
+                      // v = L^-1 k* are built in place during the factorisation
   double* part;       // partial sums, see OI_PART_*
   const double* xyt;  // n x 3 site coordinates (device)
   const double* r;    // n site residuals v = D^-1 P^T (y - mX) (device)
@@ -64,7 +65,8 @@ struct OiCell {
 #define OI_PART_GRAD(ntile) 0              // 5 per tile: s0 s1 s2 sK2 trace
 #define OI_PART_QUAD(ntile) (5 * (ntile))  // T: r_k . alpha_k
 #define OI_PART_LOGDET(ntile, T) (5 * (ntile) + (T))  // T: sum log diag(L_kk)
-#define OI_PART_SIZE(ntile, T) (5 * (ntile) + 2 * (T))
+#define OI_PART_PRED(ntile, T) (5 * (ntile) + 2 * (T))  // 3 per block: z.z, z.v, v.v
+#define OI_PART_SIZE(ntile, T) (5 * (ntile) + 5 * (T))
 
 // results inside OiCell::out
 //   eval   : [0] nlZ, [1..6] dnlZ
@@ -84,11 +86,9 @@ int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, in
                          int kbeg, int with_trtri, void* stream);
 int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
                          int with_trtri, void* stream);
-int oi_launch_zvec(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                          void* stream);
-int oi_launch_predict(const OiCell* cells, const int32_t* list, int ncell, void* stream);
 int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, void* stream);
 // r[a] = y[a] - (mX ? mX[a] : 1.0 * mean)
 int oi_set_debug(int on);

@@ -654,7 +654,6 @@ class Engine {
     HIPC(hipMemsetAsync((int32_t*)d_stat_.p + gr.s0, 0, gr.cap * 4, gst));
     const int32_t* dl_all = gr.dl;
     const int32_t* dl_ev = gr.dl + capG_;
-    const int32_t* dl_pr = gr.dl + 2 * capG_;
     const OiCell* dc = dc_;
 
     gr.ev_kind.clear();
@@ -719,22 +718,18 @@ class Engine {
     }
     cur_j = -1;
     cur_cells = ne;
-    mark(K_ZVEC, false);
-    rc |= oi_launch_zvec(dc, dl_ev, ne, maxTe, gst);
-    mark(K_ZVEC, true);
+    // z = L^-1 r was built during the factorisation (k_diag_factor / panels)
     mark(K_AVEC, false);
     rc |= oi_launch_avec(dc, dl_ev, ne, maxTe, gst);
     mark(K_AVEC, true);
     mark(K_LAUUM, false);
     rc |= oi_launch_lauum_grad(dc, dl_ev, ne, maxTe, gst);
     mark(K_LAUUM, true);
+    // nlZ / dnlZ of the fitting cells and fs / sd / lZ of the predicting ones
+    cur_cells = na;
     mark(K_FINAL, false);
-    rc |= oi_launch_finalize(dc, dl_ev, ne, gst);
+    rc |= oi_launch_finalize(dc, dl_all, na, gst);
     mark(K_FINAL, true);
-    cur_cells = np_;
-    mark(K_PRED, false);
-    rc |= oi_launch_predict(dc, dl_pr, np_, gst);
-    mark(K_PRED, true);
     if (rc) throw HipError(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     HIPC(hipMemcpyAsync(hres_ + (size_t)gr.s0 * OI_OUT_N, (double*)d_res_.p + (size_t)gr.s0 * OI_OUT_N,
                         (size_t)gr.cap * OI_OUT_N * 8, hipMemcpyDeviceToHost, gst));

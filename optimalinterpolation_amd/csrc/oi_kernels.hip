@@ -16,13 +16,16 @@
 //   k_chol_panel(j, kbeg = j-1), j odd: finishes column j / W row j with two
 //                  products per tile, look-ahead of tile j+1       (both) 2 n^3/3
 //                  (kbeg = 0: the one-column scheme, OI_PANEL=1)
-//   k_zvec/k_avec  z = W r, alpha = W^T z  (alpha = K^-1 r, GPR:127)          O(n^2)
+//   (forward substitution z = L^-1 r runs inside the factorisation: k_diag_factor
+//                  applies Dinv_jj to block j, the panels subtract L_ij z_j)
+//   k_avec         alpha = W^T z  (alpha = K^-1 r, GPR:127)                   O(n^2)
 //   k_lauum_grad1  K^-1 = W^T W, one tile per workgroup, fused with the
 //                  gradient traces sum((K^-1 - alpha alpha^T) o dK_j); K and
 //                  dK_j are regenerated from coordinates (GPR:130-138)         n^3/3
 //   k_finalize     nlZ and dnlZ (GPR:128, GPR:131-138), fixed-order sums
-// Predict (GPR:173-182): k_build, the Cholesky, then k_predict (two triangular
-// solves per cell + fs / sd / lZ).
+// Predict (GPR:173-182): k_build (also k*), the Cholesky with the forward
+// substitution of r and k* folded in, then k_finalize (fs = mean + v.z,
+// sd = sqrt(sf2 - v.v), lZ from z.z): no separate triangular solves.
 //
 // Every reduction has a fixed order that depends only on the cell, so a
 // cell's results are bitwise independent of the batch it runs in.
@@ -149,6 +152,26 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
   // (sf2 + sn2), once sf2 + sn2 rounds to sf2 (sn2 = 0 included) and takes
   // the LinAlgError branch (GPR:139-140); the m x m site form would not notice.
   if (x == 0 && t == 0 && c.n_obs > n && sf2 + sn2 == sf2) *c.status = OI_NOT_PD;
+  if (i == j && t < NB) {
+    // right-hand sides of the forward substitution run inside the
+    // factorisation: z = r (site residuals), and for predict v = k* = D kd*
+    // (GPR:174, cdist of scaled coordinates)
+    const int a = i * NB + t;
+    c.vec[a] = a < n ? c.r[a] : 0.0;
+    if (c.mode == OI_MODE_PREDICT) {
+      double kv = 0.0;
+      if (a < n) {
+        const double xs0 = (SQRT3 * c.xs[0]) / c.hyp[0], xs1 = (SQRT3 * c.xs[1]) / c.hyp[1],
+                     xs2 = (SQRT3 * c.xs[2]) / c.hyp[2];
+        const double d0 = (SQRT3 * c.xyt[3 * a]) / c.hyp[0] - xs0;
+        const double d1 = (SQRT3 * c.xyt[3 * a + 1]) / c.hyp[1] - xs1;
+        const double d2 = (SQRT3 * c.xyt[3 * a + 2]) / c.hyp[2] - xs2;
+        const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        kv = c.dw[a] * (sf2 * ((1.0 + Q) * exp(-Q)));
+      }
+      c.vec[3 * c.T * NB + a] = kv;
+    }
+  }
   double* Y = tileL(c, i, j);
   for (int e = t; e < OI_TILE; e += 256) {
     int r = e & 63, cc = e >> 6, a = i * NB + r, b = j * NB + cc;
@@ -321,6 +344,37 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
   double* Dj = tileD(c, j);
 #pragma unroll
   for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
+  // forward substitution, block j: z_j = Dinv_jj (r_j - sum_{k<j} L_jk z_k) -- the
+  // panels already subtracted the sum -- and v_j likewise for predict (k* rhs)
+  {
+    const bool pred = c.mode == OI_MODE_PREDICT;
+    double* zj = c.vec + j * NB;
+    double* vj = c.vec + 3 * c.T * NB + j * NB;
+    Tt[r] = zj[r];
+    Tt[NB + r] = pred ? vj[r] : 0.0;
+    __syncthreads();
+    double zn = 0.0, vn = 0.0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      zn = fma(R[q], Tt[q], zn);
+      vn = fma(R[q], Tt[NB + q], vn);
+    }
+    zj[r] = zn;
+    if (pred) vj[r] = vn;
+    double zz = zn * zn, zv = zn * vn, vv = vn * vn;
+    for (int o = 32; o >= 1; o >>= 1) {
+      zz += __shfl_down(zz, o, 64);
+      zv += __shfl_down(zv, o, 64);
+      vv += __shfl_down(vv, o, 64);
+    }
+    if (r == 0) {
+      double* pp = c.part + OI_PART_PRED(c.T * (c.T + 1) / 2, c.T) + 3 * j;
+      pp[0] = zz;
+      pp[1] = zv;
+      pp[2] = vv;
+    }
+    __syncthreads();  // Tt is reused below
+  }
   if (c.mode == OI_MODE_EVAL) {
 #pragma unroll
     for (int q = 0; q < NB; ++q) Tt[q * 65 + r] = R[q];  // Tt[c][r] = Inv[r][c]
@@ -402,6 +456,43 @@ __device__ __forceinline__ unsigned pad_skip(int m0, int n0, int mlim, int nlim)
   return s;
 }
 
+#define XLD 65  // LDS row stride of a staged 64x64 tile (doubles)
+
+// Forward substitution inside the factorisation: once tile L_ij (i > j) is
+// final, z_i -= L_ij z_j (and v_i -= L_ij v_j for predict; z_j, v_j final since
+// k_diag_factor(j)).  L_ij is staged in LDS as X[col * ld + row]; partial sums
+// over NTHREADS/64 column groups are combined in a fixed order (red must not
+// alias X).  Launch order makes the updates of z_i sequential in j.
+template <int NTHREADS>
+__device__ __forceinline__ void fwd_update(const OiCell& c, const double* X, int ld, int i, int j,
+                                           double* red) {
+  constexpr int G = NTHREADS / 64, CW = NB / G;
+  const bool pred = c.mode == OI_MODE_PREDICT;
+  const int t = threadIdx.x, row = t & 63, grp = t >> 6;
+  const double* zj = c.vec + j * NB;
+  const double* vj = c.vec + 3 * c.T * NB + j * NB;
+  double sz = 0.0, sv = 0.0;
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    const int col = grp * CW + q;
+    const double l = X[col * ld + row];
+    sz = fma(l, zj[col], sz);
+    if (pred) sv = fma(l, vj[col], sv);
+  }
+  red[grp * NB + row] = sz;
+  red[(G + grp) * NB + row] = sv;
+  __syncthreads();
+  if (t < NB) {
+    double a = 0.0, b = 0.0;
+    for (int g = 0; g < G; ++g) {
+      a += red[g * NB + t];
+      b += red[(G + g) * NB + t];
+    }
+    c.vec[i * NB + t] -= a;
+    if (pred) c.vec[3 * c.T * NB + i * NB + t] -= b;
+  }
+}
+
 // --------------------------------------------------- k_chol_panel(j)
 // One 256-thread workgroup per output tile; logical slots of a cell:
 //   x <  T-1-j : tile (i = j+1+x, j) of the factor, one GEMM loop:
@@ -442,9 +533,14 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
     double* Y = tileL(c, i, j);
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < 4; ++r) {
           Y[acc1_row(mb, r) * NB + acc1_col(nb)] = acc.c[mb][nb][r];  // L_ij, column-major
+          lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // staged: X[col*XLD + row]
+        }
+    __syncthreads();
+    fwd_update<256>(c, lds, XLD, i, j, lds + NB * XLD);
     if (x != 0) return;
+    __syncthreads();  // the staged tile is read before the look-ahead reuses lds
     // ---- look-ahead: diagonal tile j+1 = i.
     // S_d = A_ii - L_ij L_ij^T - sum_{k<j} L_ik L_ik^T; the first product uses
     // this workgroup's own L_ij, written k-major (X[c][m] = L_ij[m][c] = acc
@@ -522,7 +618,6 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
 //                              by k_chol_panel(j+1, kbeg=j))
 // Accumulators come out transposed with respect to the tile storage, so each
 // 64x64 half goes through LDS and is written back with coalesced 16 B rows.
-#define XLD 65  // LDS row stride of a staged 64x64 tile (doubles)
 enum { EMIT_STORE = 0, EMIT_SUB = 1, EMIT_NEG = 2 };
 
 // dst[n*64 + m] (op)= D_h[m][n] for the 64x64 half h of a gemm2 accumulator.
@@ -587,7 +682,8 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
       gemm2_kmajor<true>(acc, lds, j + 1, fpair, pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim));
     else
       gemm2_kmajor<false>(acc, lds, j + 1, fpair);
-    emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij
+    emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij (staged in lds as X[col*XLD+row])
+    fwd_update<GEMM_THREADS>(c, lds, XLD, i, j, lds + NB * XLD);
     if (x != 0) {
       emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1
       return;
@@ -631,41 +727,6 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
     gemm2_kmajor<false>(acc, lds, j - jj, wpair);
   emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);           // W_j,jj (row-major)
   if (has_next) emit_half(acc, 1, lds, tileW(c, j + 1, jj), EMIT_NEG);  // Vneg
-}
-
-// ------------------------------------------------------------- k_zvec
-// z_i = sum_{k<=i} W_ik r_k   (one workgroup per (cell, block row i))
-__global__ __launch_bounds__(256) void k_zvec(const OiCell* __restrict__ cells,
-                                              const int32_t* __restrict__ list, int gx,
-                                              int ncell) {
-  int ci, i;
-  if (!xcd_cell_slot(gx, ncell, ci, i)) return;
-  const OiCell& c = cells[list[ci]];
-  if (i >= c.T || *c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
-  // lane pair (t & 31) covers columns 2(t&31), +1 of rows 8p + (t >> 5):
-  // each load instruction reads two whole 512 B rows (coalesced).
-  typedef double dv2 __attribute__((ext_vector_type(2)));
-  const int t = threadIdx.x, h = t >> 5, cp = (t & 31) * 2, n = c.n;
-  double s[8];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) s[p] = 0.0;
-  for (int k = 0; k <= i; ++k) {
-    const int b = k * NB + cp;
-    const double r0 = b < n ? c.r[b] : 0.0, r1 = b + 1 < n ? c.r[b + 1] : 0.0;
-    const double* Wt = tileW(c, i, k) + cp;
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const dv2 w = *(const dv2*)(Wt + (8 * p + h) * NB);
-      s[p] = fma(w.y, r1, fma(w.x, r0, s[p]));
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < 8; ++p)
-    for (int o = 16; o >= 1; o >>= 1) s[p] += __shfl_xor(s[p], o, 64);
-  if ((t & 31) == 0) {
-#pragma unroll
-    for (int p = 0; p < 8; ++p) c.vec[i * NB + 8 * p + h] = s[p];
-  }
 }
 
 // ------------------------------------------------------------- k_avec
@@ -801,9 +862,32 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
 __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cells,
                                                   const int32_t* __restrict__ list) {
   const OiCell& c = cells[list[blockIdx.x]];
-  if (c.mode != OI_MODE_EVAL) return;
   __shared__ double red[4 * 7];
   const int t = threadIdx.x, T = c.T, ntile = T * (T + 1) / 2;
+  if (c.mode == OI_MODE_PREDICT) {
+    // GPR:178-182 from the forward substitution run inside the factorisation:
+    // z = L^-1 r, v = L^-1 k*: k*^T K^-1 r = v.z, k*^T K^-1 k* = v.v, r^T K^-1 r = z.z
+    if (*c.status != OI_OK) {
+      if (t < 3) c.out[t] = NAN;
+      return;
+    }
+    double p[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = t; k < T; k += 256) {
+      const double* pp = c.part + OI_PART_PRED(ntile, T) + 3 * k;
+      p[0] += pp[0];
+      p[1] += pp[1];
+      p[2] += pp[2];
+      p[3] += c.part[OI_PART_LOGDET(ntile, T) + k];
+    }
+    block_sum<4, 4>(p, red);
+    if (t == 0) {
+      const double sf2 = c.hyp[3], sn2 = c.hyp[4], nm = (double)(c.n_obs - c.n);
+      c.out[0] = c.mean + p[1];
+      c.out[1] = sqrt(sf2 - p[2]);
+      c.out[2] = ((-(p[0] + c.ssw / sn2)) / 2 - (p[3] + (nm / 2) * log(sn2))) - (c.n_obs * LOG2PI) / 2;
+    }
+    return;
+  }
   const int nslot = ntile;
   if (*c.status != OI_OK) {
     if (t < 7) c.out[t] = INFINITY;
@@ -829,121 +913,6 @@ __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cel
     c.out[4] = v[3] / 2;
     c.out[5] = sn2 * ((v[4] + nm / sn2) - c.ssw / (sn2 * sn2));
     c.out[6] = 0.0;
-  }
-}
-
-// ----------------------------------------------------------- k_predict
-// GPR:173-182 for one cell per workgroup, given L and Dinv:
-//   z = L^-1 r, v = L^-1 k*, alpha = L^-T z,
-//   fs = mean + k*.alpha, sd = sqrt(sf2 - v.v), lZ = -r.alpha/2 - sum log L_aa - n log(2pi)/2
-__global__ __launch_bounds__(256) void k_predict(const OiCell* __restrict__ cells,
-                                                 const int32_t* __restrict__ list) {
-  const OiCell& c = cells[list[blockIdx.x]];
-  if (c.mode != OI_MODE_PREDICT) return;
-  const int t = threadIdx.x, T = c.T, n = c.n;
-  if (*c.status != OI_OK) {
-    if (t < 3) c.out[t] = NAN;
-    return;
-  }
-  __shared__ double red2[4][2][NB + 1];
-  __shared__ double tv[2][NB];
-  __shared__ double red[4 * 5];
-  double* z = c.vec;
-  double* alpha = c.vec + T * NB;
-  double* ks = c.vec + 2 * T * NB;
-  double* v = c.vec + 3 * T * NB;
-  const double sf2 = c.hyp[3];
-  // k* (GPR:174): cdist of scaled coordinates
-  {
-    const double xs0 = (SQRT3 * c.xs[0]) / c.hyp[0], xs1 = (SQRT3 * c.xs[1]) / c.hyp[1],
-                 xs2 = (SQRT3 * c.xs[2]) / c.hyp[2];
-    for (int a = t; a < T * NB; a += 256) {
-      double kv = 0.0;
-      if (a < n) {
-        double d0 = (SQRT3 * c.xyt[3 * a]) / c.hyp[0] - xs0;
-        double d1 = (SQRT3 * c.xyt[3 * a + 1]) / c.hyp[1] - xs1;
-        double d2 = (SQRT3 * c.xyt[3 * a + 2]) / c.hyp[2] - xs2;
-        double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-        kv = c.dw[a] * (sf2 * ((1.0 + Q) * exp(-Q)));  // D kd* (k* = P kd*)
-      }
-      ks[a] = kv;
-    }
-  }
-  __syncthreads();
-  // forward: [z v]_i = Dinv_ii ([r ks]_i - sum_{k<i} L_ik [z v]_k)
-  const int m = t & 63, cq = t >> 6;
-  for (int i = 0; i < T; ++i) {
-    double s0 = 0.0, s1 = 0.0;
-    for (int k = 0; k < i; ++k) {
-      const double* Lt = c.L + (((size_t)i * (i + 1) / 2) + k) * OI_TILE;
-      for (int cc = 16 * cq; cc < 16 * cq + 16; ++cc) {
-        const double l = Lt[cc * NB + m];
-        s0 += l * z[k * NB + cc];
-        s1 += l * v[k * NB + cc];
-      }
-    }
-    red2[cq][0][m] = s0;
-    red2[cq][1][m] = s1;
-    __syncthreads();
-    if (t < NB) {
-      const int b = i * NB + t;
-      const double rb = b < n ? c.r[b] : 0.0;
-      tv[0][t] = rb - (((red2[0][0][t] + red2[1][0][t]) + red2[2][0][t]) + red2[3][0][t]);
-      tv[1][t] = ks[b] - (((red2[0][1][t] + red2[1][1][t]) + red2[2][1][t]) + red2[3][1][t]);
-    }
-    __syncthreads();
-    const double* Dt = c.Dinv + (size_t)i * OI_TILE;
-    s0 = 0.0;
-    s1 = 0.0;
-    for (int cc = 16 * cq; cc < 16 * cq + 16; ++cc) {
-      const double d = Dt[cc * NB + m];
-      s0 += d * tv[0][cc];
-      s1 += d * tv[1][cc];
-    }
-    red2[cq][0][m] = s0;
-    red2[cq][1][m] = s1;
-    __syncthreads();
-    if (t < NB) {
-      z[i * NB + t] = ((red2[0][0][t] + red2[1][0][t]) + red2[2][0][t]) + red2[3][0][t];
-      v[i * NB + t] = ((red2[0][1][t] + red2[1][1][t]) + red2[2][1][t]) + red2[3][1][t];
-    }
-    __syncthreads();
-  }
-  // backward: alpha_i = Dinv_ii^T (z_i - sum_{k>i} L_ki^T alpha_k)
-  const int mr = t >> 2, q = t & 3;
-  for (int i = T - 1; i >= 0; --i) {
-    double s0 = 0.0;
-    for (int k = i + 1; k < T; ++k) {
-      const double* Lt = c.L + (((size_t)k * (k + 1) / 2) + i) * OI_TILE;
-      for (int cc = 16 * q; cc < 16 * q + 16; ++cc) s0 += Lt[mr * NB + cc] * alpha[k * NB + cc];
-    }
-    s0 += __shfl_xor(s0, 1, 64);
-    s0 += __shfl_xor(s0, 2, 64);
-    if (q == 0) tv[0][mr] = z[i * NB + mr] - s0;
-    __syncthreads();
-    const double* Dt = c.Dinv + (size_t)i * OI_TILE;
-    double s1 = 0.0;
-    for (int cc = 16 * q; cc < 16 * q + 16; ++cc) s1 += Dt[mr * NB + cc] * tv[0][cc];
-    s1 += __shfl_xor(s1, 1, 64);
-    s1 += __shfl_xor(s1, 2, 64);
-    if (q == 0) alpha[i * NB + mr] = s1;
-    __syncthreads();
-  }
-  // reductions: k*.alpha, v.v, r.alpha, sum log diag L
-  double acc5[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int a = t; a < n; a += 256) {
-    acc5[0] += ks[a] * alpha[a];
-    acc5[1] += v[a] * v[a];
-    acc5[2] += c.r[a] * alpha[a];
-    const int bi = a >> 6, bm = a & 63;
-    acc5[3] += log(c.L[(((size_t)bi * (bi + 1) / 2) + bi) * OI_TILE + bm * NB + bm]);
-  }
-  block_sum<4, 4>(acc5, red);
-  if (t == 0) {
-    const double sn2 = c.hyp[4], nm = (double)(c.n_obs - n);
-    c.out[0] = c.mean + acc5[0];
-    c.out[1] = sqrt(sf2 - acc5[1]);
-    c.out[2] = ((-(acc5[2] + c.ssw / sn2)) / 2 - (acc5[3] + (nm / 2) * log(sn2))) - (c.n_obs * LOG2PI) / 2;
   }
 }
 
@@ -1137,14 +1106,6 @@ extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, in
   return ret();
 }
 
-extern "C" int oi_launch_zvec(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                              void* stream) {
-  if (ncell <= 0 || maxT <= 0) return 0;
-  hipLaunchKernelGGL(k_zvec, dim3(grid1(maxT, ncell)), dim3(256), 0, S(stream), cells, list, maxT,
-                     ncell);
-  return ret();
-}
-
 extern "C" int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                               void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
@@ -1159,13 +1120,6 @@ extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, in
   const int gx = maxT * (maxT + 1) / 2;
   hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,
                      ncell);
-  return ret();
-}
-
-extern "C" int oi_launch_predict(const OiCell* cells, const int32_t* list, int ncell,
-                                 void* stream) {
-  if (ncell <= 0) return 0;
-  hipLaunchKernelGGL(k_predict, dim3(ncell), dim3(256), 0, S(stream), cells, list);
   return ret();
 }
 
