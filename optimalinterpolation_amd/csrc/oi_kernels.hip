@@ -460,19 +460,39 @@ __device__ __forceinline__ unsigned pad_skip(int m0, int n0, int mlim, int nlim)
 
 // Forward substitution inside the factorisation: once tile L_ij (i > j) is
 // final, z_i -= L_ij z_j (and v_i -= L_ij v_j for predict; z_j, v_j final since
-// k_diag_factor(j)).  L_ij is staged in LDS as X[col * ld + row]; partial sums
-// over NTHREADS/64 column groups are combined in a fixed order (red must not
-// alias X).  Launch order makes the updates of z_i sequential in j.
+// k_diag_factor(j)).  fwd_preload, issued before the tile's GEMM loop so its
+// latency hides behind it, gives thread t one value: z_i[t] (t < 64), z_j
+// (64..127), v_i (128..191), v_j (192..255).  fwd_update then stages z_j, v_j
+// in LDS, forms L_ij [z_j v_j] from the tile staged as X[col * ld + row] with
+// partial sums over NTHREADS/64 column groups combined in a fixed order, and
+// writes z_i, v_i.  scratch (>= (2 * NTHREADS/64 + 2) * 64 doubles) must not
+// alias X.  Launch order makes the updates of z_i sequential in j.
+__device__ __forceinline__ double fwd_preload(const OiCell& c, int i, int j) {
+  const int t = threadIdx.x;
+  const bool pred = c.mode == OI_MODE_PREDICT;
+  const double* z = c.vec;
+  const double* v = c.vec + 3 * c.T * NB;
+  if (t < 64) return z[i * NB + t];
+  if (t < 128) return z[j * NB + t - 64];
+  if (pred && t < 192) return v[i * NB + t - 128];
+  if (pred && t < 256) return v[j * NB + t - 192];
+  return 0.0;
+}
+
 template <int NTHREADS>
-__device__ __forceinline__ void fwd_update(const OiCell& c, const double* X, int ld, int i, int j,
-                                           double* red) {
+__device__ __forceinline__ void fwd_update(const OiCell& c, const double* X, int ld, int i, double pre,
+                                           double* scratch) {
   constexpr int G = NTHREADS / 64, CW = NB / G;
   const bool pred = c.mode == OI_MODE_PREDICT;
   const int t = threadIdx.x, row = t & 63, grp = t >> 6;
-  const double* zj = c.vec + j * NB;
-  const double* vj = c.vec + 3 * c.T * NB + j * NB;
+  double* red = scratch;
+  double* zj = scratch + 2 * G * NB;
+  double* vj = zj + NB;
+  if (t >= 64 && t < 128) zj[t - 64] = pre;
+  if (t >= 192 && t < 256) vj[t - 192] = pre;
+  __syncthreads();
   double sz = 0.0, sv = 0.0;
-#pragma unroll
+#pragma unroll 4
   for (int q = 0; q < CW; ++q) {
     const int col = grp * CW + q;
     const double l = X[col * ld + row];
@@ -482,14 +502,11 @@ __device__ __forceinline__ void fwd_update(const OiCell& c, const double* X, int
   red[grp * NB + row] = sz;
   red[(G + grp) * NB + row] = sv;
   __syncthreads();
-  if (t < NB) {
-    double a = 0.0, b = 0.0;
-    for (int g = 0; g < G; ++g) {
-      a += red[g * NB + t];
-      b += red[(G + g) * NB + t];
-    }
-    c.vec[i * NB + t] -= a;
-    if (pred) c.vec[3 * c.T * NB + i * NB + t] -= b;
+  if (t < 64 || (pred && t >= 128 && t < 192)) {
+    const int h = t < 64 ? 0 : 1;
+    double a = 0.0;
+    for (int g = 0; g < G; ++g) a += red[(h * G + g) * NB + row];
+    c.vec[(h ? 3 * c.T * NB : 0) + i * NB + row] = pre - a;
   }
 }
 
@@ -526,6 +543,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
       b = tileL(c, i, k);  // k == j: A_ij, already holding A_ij - sum_{k<kbeg} L_ik L_jk^T
     };
+    const double pre = fwd_preload(c, i, j);
     if (i == T - 1 && rT < NB)  // n = row of block row i
       gemm1_kmajor<true>(acc, lds, 4 * (j + 1 - kbeg), pad_skip(32 * wr, 32 * wc, NB, rT), fpair);
     else
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
           lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // staged: X[col*XLD + row]
         }
     __syncthreads();
-    fwd_update<256>(c, lds, XLD, i, j, lds + NB * XLD);
+    fwd_update<256>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) return;
     __syncthreads();  // the staged tile is read before the look-ahead reuses lds
     // ---- look-ahead: diagonal tile j+1 = i.
@@ -678,12 +696,13 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
     };
     // m = row of block row i; half 1's n = column of block column j+1
     const int mlim = i == T - 1 ? rT : NB, nlim = (wc >= 2 && j + 1 == T - 1) ? rT : NB;
+    const double pre = fwd_preload(c, i, j);
     if (mlim < NB || nlim < NB)
       gemm2_kmajor<true>(acc, lds, j + 1, fpair, pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim));
     else
       gemm2_kmajor<false>(acc, lds, j + 1, fpair);
     emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij (staged in lds as X[col*XLD+row])
-    fwd_update<GEMM_THREADS>(c, lds, XLD, i, j, lds + NB * XLD);
+    fwd_update<GEMM_THREADS>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) {
       emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1
       return;
