@@ -654,7 +654,8 @@ def main():
     # one-shot call on 8 small cells -- not a step
     if not args.no_prime:
         prime = synthetic.make_cells([300] * 8, seed=12345)
-        _lib.gpr_batch(prime.xyt, prime.z, prime.offs, prime.xs, prime.mean, x0=X0, opt=True, device=gpu)
+        _lib.gpr_batch(prime.xyt, prime.z, prime.offs, prime.xs, prime.mean, x0=X0, opt=True, device=gpu,
+                       profile=True)
     single = args.workload == 'single'
     sess = None if single else _lib.Session(device=gpu, device_inputs=True, profile=True)
     if single:  # config 1: blocking one-shot calls (per-cell latency)
@@ -665,6 +666,7 @@ def main():
         for item in dev_warm:
             submit(sess, item)
         sess.wait(-1)
+    prof_untimed = _lib.profile_json()['kernels']  # priming + warmup launches (rocprof sees them too)
     _lib.profile_reset()
     log("warmup done; timing")
 
@@ -734,6 +736,14 @@ def main():
             "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
             "failed_cells": int(np.sum(status != 0)), "timed_s": round(dt, 3),
             "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float))}
+    dom = line["roofline"]["kernel"]
+    pu, pt = prof_untimed.get(dom, {"launches": 0, "total_ms": 0.0}), prof["kernels"][dom]
+    nall = pu["launches"] + pt["launches"]
+    line["roofline"]["rocprof_crosscheck"] = {
+        "launches_incl_untimed": nall,
+        "avg_launch_ms_incl_untimed": (pu["total_ms"] + pt["total_ms"]) / max(nall, 1),
+        "note": "HIP-event average over every launch of the process (priming + warmup + timed), the set a "
+                "rocprofv3 --kernel-trace --stats run of this command averages over"}
     if done_k != args.steps or truncated:
         line.update({"truncated": True, "steps_requested": args.steps})
     if rank == 0:

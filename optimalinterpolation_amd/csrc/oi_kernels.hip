@@ -384,6 +384,188 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
   }
 }
 
+// ------------------------------------------ k_diag_factor16(j) (default)
+// The same contract as k_diag_factor, blocked by 16 columns so the serial
+// (v_readlane-broadcast) work shrinks and the MFMA unit -- idle in the
+// 32-blocked kernel -- does the rest.  One 64-lane wave per cell, lane r
+// holding row r of the tile in registers:
+//   potrf: for each 16-column panel J, the panel is factored serially (<= 15
+//          broadcasts per column instead of <= 63), then the trailing block
+//          update A_IK -= P_I P_K^T (I >= K > J) runs on v_mfma_f64_16x16x4f64
+//          through LDS;
+//   inverse: the four 16x16 diagonal blocks are inverted at once (trti2 in
+//          LAPACK dtrti2 order, broadcasts within 16-lane groups), then the
+//          off-diagonal blocks Inv_IJ = -Inv_II sum_{K=J}^{I-1} L_IK Inv_KJ by
+//          levels I - J = 1, 2, 3 on the MFMA unit.
+// LDS: Ls (the factor, row-major, stride 65) and Iv (the inverse, column-major
+// -- Iv[c*65 + r] = Inv[r][c] -- stride 65); the potrf panel (in Iv) and the
+// trailing-update results (in Ls) alias them.
+#define D16_LD 65
+// acc (16x16, lane l holds rows (l>>4) + 4q, column l&15) += A B with
+// A[m][k] = Am[m * la + k] (or Am[k * la + m] if a_km) and B[k][n] = Bt[n * lb + k]
+__device__ __forceinline__ void mfma16x16(d4& acc, const double* Am, int la, bool a_km, const double* Bt,
+                                          int lb) {
+  const int l = threadIdx.x & 63, fr = l & 15, fk = l >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 4 * kk + fk;
+    const double a = a_km ? Am[k * la + fr] : Am[fr * la + k];
+    acc = MFMA64(a, Bt[fr * lb + k], acc);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__ cells,
+                                                     const int32_t* __restrict__ list, int j) {
+  __shared__ double Ls[NB * D16_LD];
+  __shared__ double Iv[NB * D16_LD];
+  __shared__ double Xs[16 * 17];
+  const OiCell& c = cells[list[blockIdx.x]];
+  if (j >= c.T || *c.status != OI_OK) return;
+  const int r = threadIdx.x, fr = r & 15, fk = r >> 4, blk = r >> 4;
+  double* Y = tileL(c, j, j);
+  double R[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) R[q] = Y[q * NB + r];  // row r of the column-major tile
+  bool ok = true;
+  // ---------------- potrf by 16-column panels
+#pragma unroll
+  for (int J = 0; J < 4; ++J) {
+    const int c0 = 16 * J;
+#pragma unroll
+    for (int cc = c0; cc < c0 + 16; ++cc) {
+      const double d = rdlane(R[cc], cc);
+      ok = ok && !(d <= 0.0);
+      const double l = sqrt(d);
+      const double lr = r > cc ? R[cc] / l : 0.0;
+      R[cc] = r > cc ? lr : (r == cc ? l : R[cc]);
+#pragma unroll
+      for (int s2 = cc + 1; s2 < c0 + 16; ++s2) R[s2] -= lr * rdlane(R[cc], s2);
+    }
+    if (J == 3) break;
+    // trailing update: A_IK -= P_I P_K^T for J < K <= I, P = rows of panel J
+    double* P = Iv;                 // 64 x 17
+    double* U = Ls;                 // results: U[row * 49 + (s - c0 - 16)] (Ls is free until the end)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) P[r * 17 + q] = r > c0 + q ? R[c0 + q] : (r == c0 + q ? R[c0 + q] : 0.0);
+    __syncthreads();
+#pragma unroll
+    for (int I = J + 1; I < 4; ++I)
+#pragma unroll
+      for (int K = J + 1; K <= I; ++K) {
+        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+        mfma16x16(acc, P + 16 * I * 17, 17, false, P + 16 * K * 17, 17);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) U[(16 * I + fk + 4 * q) * 49 + 16 * (K - J - 1) + fr] = acc[q];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = c0 + 16; s2 < NB; ++s2)
+      if ((s2 >> 4) <= blk) R[s2] -= U[r * 49 + (s2 - c0 - 16)];
+    __syncthreads();  // P / U are rewritten by the next panel
+  }
+  if (!ok) {
+    if (r == 0) {
+      *c.status = OI_NOT_PD;
+      if (g_debug)
+        printf("oi debug: not PD: cell n=%d T=%d diagonal tile j=%d hyp %g %g %g %g %g\n", c.n, c.T,
+               j, c.hyp[0], c.hyp[1], c.hyp[2], c.hyp[3], c.hyp[4]);
+    }
+    return;
+  }
+  double lg = 0.0;
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (q > r) R[q] = 0.0;                                   // clear the upper part
+    if (q == r) lg = (j * NB + r < c.n) ? log(R[q]) : 0.0;   // log L_rr
+    Y[q * NB + r] = R[q];                                    // L_jj, column-major
+    Ls[r * D16_LD + q] = R[q];                               // row-major copy for the MFMA steps
+  }
+  for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
+  if (r == 0) {
+    const int ntile = c.T * (c.T + 1) / 2;
+    c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
+  }
+  // ---------------- inverse: four diagonal 16x16 blocks at once (dtrti2 order)
+  double D[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q)  // D[q] = L[r][16 blk + q]
+    D[q] = blk == 0 ? R[q] : blk == 1 ? R[16 + q] : blk == 2 ? R[32 + q] : R[48 + q];
+#pragma unroll
+  for (int cc = 15; cc >= 0; --cc) {
+    const double ajj = 1.0 / __shfl(D[cc], cc, 16);
+    double x = 0.0;
+#pragma unroll
+    for (int k = cc + 1; k < 16; ++k) x += D[k] * __shfl(D[cc], k, 16);
+    D[cc] = fr > cc ? -ajj * x : (fr == cc ? ajj : D[cc]);
+  }
+  __syncthreads();  // Iv held the potrf scratch
+#pragma unroll
+  for (int q = 0; q < NB; ++q) Iv[q * D16_LD + r] = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) Iv[(16 * blk + q) * D16_LD + r] = D[q];  // Inv_II, column-major
+  __syncthreads();
+  // ---------------- off-diagonal blocks by levels: Inv_IJ = -Inv_II X, X = sum_K L_IK Inv_KJ
+#pragma unroll
+  for (int lev = 1; lev < 4; ++lev) {
+#pragma unroll
+    for (int J = 0; J + lev < 4; ++J) {
+      const int I = J + lev;
+      d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int K = J; K < I; ++K)  // A = L_IK (row-major), B = Inv_KJ: Bt[n][k] = Iv[(16J + n)*65 + 16K + k]
+        mfma16x16(acc, Ls + 16 * I * D16_LD + 16 * K, D16_LD, false, Iv + 16 * J * D16_LD + 16 * K, D16_LD);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xs[fr * 17 + fk + 4 * q] = acc[q];  // Xs[n][m] = X[m][n]
+      __syncthreads();
+      d4 y = (d4){0.0, 0.0, 0.0, 0.0};
+      // A = Inv_II: A[m][k] = Inv[16I + m][16I + k] = Iv[(16I + k)*65 + 16I + m]  (k-major)
+      mfma16x16(y, Iv + 16 * I * D16_LD + 16 * I, D16_LD, true, Xs, 17);
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Iv[(16 * J + fr) * D16_LD + 16 * I + fk + 4 * q] = -y[q];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) R[q] = Iv[q * D16_LD + r];  // row r of the inverse
+  double* Dj = tileD(c, j);
+#pragma unroll
+  for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
+  // forward substitution, block j (see k_diag_factor)
+  {
+    const bool pred = c.mode == OI_MODE_PREDICT;
+    double* zj = c.vec + j * NB;
+    double* vj = c.vec + 3 * c.T * NB + j * NB;
+    Xs[r] = zj[r];
+    Xs[NB + r] = pred ? vj[r] : 0.0;
+    __syncthreads();
+    double zn = 0.0, vn = 0.0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      zn = fma(R[q], Xs[q], zn);
+      vn = fma(R[q], Xs[NB + q], vn);
+    }
+    zj[r] = zn;
+    if (pred) vj[r] = vn;
+    double zz = zn * zn, zv = zn * vn, vv = vn * vn;
+    for (int o = 32; o >= 1; o >>= 1) {
+      zz += __shfl_down(zz, o, 64);
+      zv += __shfl_down(zv, o, 64);
+      vv += __shfl_down(vv, o, 64);
+    }
+    if (r == 0) {
+      double* pp = c.part + OI_PART_PRED(c.T * (c.T + 1) / 2, c.T) + 3 * j;
+      pp[0] = zz;
+      pp[1] = zv;
+      pp[2] = vv;
+    }
+  }
+  if (c.mode == OI_MODE_EVAL) {
+    double* Wj = tileW(c, j, j);  // row-major W = L^-1: W[q][r] = Iv[r * 65 + q]
+    for (int q = 0; q < NB; ++q) Wj[q * NB + r] = Iv[r * D16_LD + q];
+  }
+}
+
 // ----------------------------------------------------------- k_scale(j)
 // P_jk = -Dinv_jj L_jk for k < j (column-major), so that the panel tiles and
 // the row of W become single GEMM loops (no separate Dinv product per tile).
@@ -1094,7 +1276,14 @@ extern "C" int oi_launch_build(const OiCell* cells, const int32_t* list, int nce
 extern "C" int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j,
                                      void* stream) {
   if (ncell <= 0) return 0;
-  hipLaunchKernelGGL(k_diag_factor, dim3(ncell), dim3(64), 0, S(stream), cells, list, j);
+  static const int variant = [] {
+    const char* e = getenv("OI_DIAG");
+    return e ? atoi(e) : 16;
+  }();
+  if (variant == 32)  // the round-1 32-blocked kernel (A/B)
+    hipLaunchKernelGGL(k_diag_factor, dim3(ncell), dim3(64), 0, S(stream), cells, list, j);
+  else
+    hipLaunchKernelGGL(k_diag_factor16, dim3(ncell), dim3(64), 0, S(stream), cells, list, j);
   return ret();
 }
 
