@@ -401,6 +401,9 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
 // -- Iv[c*65 + r] = Inv[r][c] -- stride 65); the potrf panel (in Iv) and the
 // trailing-update results (in Ls) alias them.
 #define D16_LD 65
+// packed block slots: L_IK (I > K) and Inv_IK (I >= K) of the 4 x 4 blocks of a tile
+__device__ __forceinline__ int lb_index(int I, int K) { return I * (I - 1) / 2 + K; }
+__device__ __forceinline__ int ib_index(int I, int K) { return I * (I + 1) / 2 + K; }
 // acc (16x16, lane l holds rows (l>>4) + 4q, column l&15) += A B with
 // A[m][k] = Am[m * la + k] (or Am[k * la + m] if a_km) and B[k][n] = Bt[n * lb + k]
 __device__ __forceinline__ void mfma16x16(d4& acc, const double* Am, int la, bool a_km, const double* Bt,
@@ -416,9 +419,14 @@ __device__ __forceinline__ void mfma16x16(d4& acc, const double* Am, int la, boo
 
 __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__ cells,
                                                      const int32_t* __restrict__ list, int j) {
-  __shared__ double Ls[NB * D16_LD];
-  __shared__ double Iv[NB * D16_LD];
-  __shared__ double Xs[16 * 17];
+  // packed 16x16 blocks (row stride 17): Lb holds L_IK (I > K, 6 blocks), Ib the
+  // inverse's lower blocks Inv_IK (I >= K, 10 blocks) stored transposed (Ib[n*17 + m]
+  // = Inv[16I + m][16K + n]); the potrf panel P and update results U alias them
+  // (37 KB: four workgroups per CU)
+  __shared__ double lds16[16 * 17 * 17 + 16 * 17];
+  double* Lb = lds16;                 // 6 blocks
+  double* Ib = lds16 + 6 * 272;       // 10 blocks
+  double* Xs = lds16 + 16 * 272;      // 16 x 17
   const OiCell& c = cells[list[blockIdx.x]];
   if (j >= c.T || *c.status != OI_OK) return;
   const int r = threadIdx.x, fr = r & 15, fk = r >> 4, blk = r >> 4;
@@ -443,8 +451,8 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     }
     if (J == 3) break;
     // trailing update: A_IK -= P_I P_K^T for J < K <= I, P = rows of panel J
-    double* P = Iv;                 // 64 x 17
-    double* U = Ls;                 // results: U[row * 49 + (s - c0 - 16)] (Ls is free until the end)
+    double* P = lds16;              // 64 x 17
+    double* U = lds16 + NB * 17;    // results: U[row * 49 + (s - c0 - 16)]
 #pragma unroll
     for (int q = 0; q < 16; ++q) P[r * 17 + q] = r > c0 + q ? R[c0 + q] : (r == c0 + q ? R[c0 + q] : 0.0);
     __syncthreads();
@@ -478,8 +486,14 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     if (q > r) R[q] = 0.0;                                   // clear the upper part
     if (q == r) lg = (j * NB + r < c.n) ? log(R[q]) : 0.0;   // log L_rr
     Y[q * NB + r] = R[q];                                    // L_jj, column-major
-    Ls[r * D16_LD + q] = R[q];                               // row-major copy for the MFMA steps
   }
+  __syncthreads();  // lds16 held the potrf scratch
+#pragma unroll
+  for (int K = 0; K < 4; ++K)  // L_IK blocks (I = blk > K), row-major for the MFMA A operand
+    if (K < blk) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Lb[lb_index(blk, K) * 272 + fr * 17 + q] = R[16 * K + q];
+    }
   for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
   if (r == 0) {
     const int ntile = c.T * (c.T + 1) / 2;
@@ -498,11 +512,8 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     for (int k = cc + 1; k < 16; ++k) x += D[k] * __shfl(D[cc], k, 16);
     D[cc] = fr > cc ? -ajj * x : (fr == cc ? ajj : D[cc]);
   }
-  __syncthreads();  // Iv held the potrf scratch
 #pragma unroll
-  for (int q = 0; q < NB; ++q) Iv[q * D16_LD + r] = 0.0;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) Iv[(16 * blk + q) * D16_LD + r] = D[q];  // Inv_II, column-major
+  for (int q = 0; q < 16; ++q) Ib[ib_index(blk, blk) * 272 + q * 17 + fr] = D[q];  // Inv_II (transposed)
   __syncthreads();
   // ---------------- off-diagonal blocks by levels: Inv_IJ = -Inv_II X, X = sum_K L_IK Inv_KJ
 #pragma unroll
@@ -512,22 +523,25 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
       const int I = J + lev;
       d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int K = J; K < I; ++K)  // A = L_IK (row-major), B = Inv_KJ: Bt[n][k] = Iv[(16J + n)*65 + 16K + k]
-        mfma16x16(acc, Ls + 16 * I * D16_LD + 16 * K, D16_LD, false, Iv + 16 * J * D16_LD + 16 * K, D16_LD);
+      for (int K = J; K < I; ++K)  // A = L_IK (row-major), B = Inv_KJ: Bt[n][k] = Inv[16K + k][16J + n]
+        mfma16x16(acc, Lb + lb_index(I, K) * 272, 17, false, Ib + ib_index(K, J) * 272, 17);
 #pragma unroll
       for (int q = 0; q < 4; ++q) Xs[fr * 17 + fk + 4 * q] = acc[q];  // Xs[n][m] = X[m][n]
       __syncthreads();
       d4 y = (d4){0.0, 0.0, 0.0, 0.0};
-      // A = Inv_II: A[m][k] = Inv[16I + m][16I + k] = Iv[(16I + k)*65 + 16I + m]  (k-major)
-      mfma16x16(y, Iv + 16 * I * D16_LD + 16 * I, D16_LD, true, Xs, 17);
+      // A = Inv_II: A[m][k] = Inv[16I + m][16I + k] = Ib_II[k * 17 + m]  (k-major)
+      mfma16x16(y, Ib + ib_index(I, I) * 272, 17, true, Xs, 17);
       __syncthreads();
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Iv[(16 * J + fr) * D16_LD + 16 * I + fk + 4 * q] = -y[q];
+      for (int q = 0; q < 4; ++q) Ib[ib_index(I, J) * 272 + fr * 17 + fk + 4 * q] = -y[q];
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int q = 0; q < NB; ++q) R[q] = Iv[q * D16_LD + r];  // row r of the inverse
+  for (int q = 0; q < NB; ++q) {  // row r of the inverse: Inv[r][q] (zero above the diagonal blocks)
+    const int K = q >> 4;
+    R[q] = K <= blk ? Ib[ib_index(blk, K) * 272 + (q & 15) * 17 + fr] : 0.0;
+  }
   double* Dj = tileD(c, j);
 #pragma unroll
   for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
@@ -537,7 +551,7 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     double* zj = c.vec + j * NB;
     double* vj = c.vec + 3 * c.T * NB + j * NB;
     Xs[r] = zj[r];
-    Xs[NB + r] = pred ? vj[r] : 0.0;
+    Xs[NB + r] = pred ? vj[r] : 0.0;  // Xs has room for 272 doubles
     __syncthreads();
     double zn = 0.0, vn = 0.0;
 #pragma unroll
@@ -561,8 +575,12 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     }
   }
   if (c.mode == OI_MODE_EVAL) {
-    double* Wj = tileW(c, j, j);  // row-major W = L^-1: W[q][r] = Iv[r * 65 + q]
-    for (int q = 0; q < NB; ++q) Wj[q * NB + r] = Iv[r * D16_LD + q];
+    double* Wj = tileW(c, j, j);  // row-major W = L^-1: W[q][r] = Inv[q][r]
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NB; ++q) lds16[q * D16_LD + r] = R[q];  // lds16[c*65 + r] = Inv[r][c]
+    __syncthreads();
+    for (int q = 0; q < NB; ++q) Wj[q * NB + r] = lds16[r * D16_LD + q];
   }
 }
 

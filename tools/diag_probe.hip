@@ -1,0 +1,194 @@
+// Stage timing of the 16-blocked diagonal-tile factor (k_diag_factor16): B
+// independent SPD 64x64 tiles, one wave each, stages cut off at STAGE:
+//   0 load + store, 1 + potrf, 2 + diagonal 16x16 inverses, 3 + off-diagonal blocks.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include <vector>
+#define CHK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP error %s at %d\n",hipGetErrorString(e),__LINE__); exit(1);}}while(0)
+#define NB 64
+#define LD 65
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0)
+
+__device__ __forceinline__ double rdlane(double v, int lane) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffLL), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ void mfma16x16(d4& acc, const double* Am, int la, bool a_km, const double* Bt, int lb) {
+  const int l = threadIdx.x & 63, fr = l & 15, fk = l >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 4 * kk + fk;
+    const double a = a_km ? Am[k * la + fr] : Am[fr * la + k];
+    acc = MFMA64(a, Bt[fr * lb + k], acc);
+  }
+}
+
+template <int STAGE>
+__global__ __launch_bounds__(64) void kd(const double* A, double* L, double* Dout) {
+  __shared__ double Ls[NB * LD];
+  __shared__ double Iv[NB * LD];
+  __shared__ double Xs[16 * 17];
+  const int r = threadIdx.x, fr = r & 15, fk = r >> 4, blk = r >> 4;
+  const double* Y = A + (size_t)blockIdx.x * 4096;
+  double R[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) R[q] = Y[q * NB + r];
+  if (STAGE >= 1) {
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      const int c0 = 16 * J;
+#pragma unroll
+      for (int cc = c0; cc < c0 + 16; ++cc) {
+        const double d = rdlane(R[cc], cc);
+        const double l = sqrt(d);
+        const double lr = r > cc ? R[cc] / l : 0.0;
+        R[cc] = r > cc ? lr : (r == cc ? l : R[cc]);
+#pragma unroll
+        for (int s2 = cc + 1; s2 < c0 + 16; ++s2) R[s2] -= lr * rdlane(R[cc], s2);
+      }
+      if (J == 3) break;
+      double* P = Iv;
+      double* U = Ls;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) P[r * 17 + q] = r >= c0 + q ? R[c0 + q] : 0.0;
+      __syncthreads();
+#pragma unroll
+      for (int I = J + 1; I < 4; ++I)
+#pragma unroll
+        for (int K = J + 1; K <= I; ++K) {
+          d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+          mfma16x16(acc, P + 16 * I * 17, 17, false, P + 16 * K * 17, 17);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) U[(16 * I + fk + 4 * q) * 49 + 16 * (K - J - 1) + fr] = acc[q];
+        }
+      __syncthreads();
+#pragma unroll
+      for (int s2 = c0 + 16; s2 < NB; ++s2)
+        if ((s2 >> 4) <= blk) R[s2] -= U[r * 49 + (s2 - c0 - 16)];
+      __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      if (q > r) R[q] = 0.0;
+      Ls[r * LD + q] = R[q];
+    }
+  }
+  if (STAGE >= 2) {
+    double D[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      D[q] = blk == 0 ? R[q] : blk == 1 ? R[16 + q] : blk == 2 ? R[32 + q] : R[48 + q];
+#pragma unroll
+    for (int cc = 15; cc >= 0; --cc) {
+      const double ajj = 1.0 / __shfl(D[cc], cc, 16);
+      double x = 0.0;
+#pragma unroll
+      for (int k = cc + 1; k < 16; ++k) x += D[k] * __shfl(D[cc], k, 16);
+      D[cc] = fr > cc ? -ajj * x : (fr == cc ? ajj : D[cc]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NB; ++q) Iv[q * LD + r] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) Iv[(16 * blk + q) * LD + r] = D[q];
+    __syncthreads();
+  }
+  if (STAGE >= 3) {
+#pragma unroll
+    for (int lev = 1; lev < 4; ++lev) {
+#pragma unroll
+      for (int J = 0; J + lev < 4; ++J) {
+        const int I = J + lev;
+        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int K = J; K < I; ++K)
+          mfma16x16(acc, Ls + 16 * I * LD + 16 * K, LD, false, Iv + 16 * J * LD + 16 * K, LD);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Xs[fr * 17 + fk + 4 * q] = acc[q];
+        __syncthreads();
+        d4 y = (d4){0.0, 0.0, 0.0, 0.0};
+        mfma16x16(y, Iv + 16 * I * LD + 16 * I, LD, true, Xs, 17);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Iv[(16 * J + fr) * LD + 16 * I + fk + 4 * q] = -y[q];
+      }
+      __syncthreads();
+    }
+  }
+  if (STAGE >= 2) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) R[q] = Iv[q * LD + r];
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) Dout[(size_t)blockIdx.x * 4096 + q * NB + r] = R[q];
+  if (STAGE >= 4) {  // the real kernel's epilogue: log-det, forward substitution, W store
+    double lg = log(Ls[r * LD + r]);
+    for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
+    double* zj = L + (size_t)blockIdx.x * 4096;  // reuse L as the vector area
+    Xs[r] = zj[r];
+    __syncthreads();
+    double zn = 0.0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) zn = fma(R[q], Xs[q], zn);
+    zj[r] = zn + (r == 0 ? lg : 0.0);
+    double* Wj = L + (size_t)blockIdx.x * 4096 + 64;
+    for (int q = 0; q < 63; ++q) Wj[q * NB + r] = Iv[r * LD + q];
+  }
+}
+
+int main() {
+  const int BMAX = 2048;
+  std::vector<double> h((size_t)BMAX * 4096);
+  srand(1);
+  for (int b = 0; b < BMAX; ++b) {  // SPD: M = B B^T / 64 + I
+    std::vector<double> Bm(4096);
+    for (auto& v : Bm) v = (rand() / (double)RAND_MAX) - 0.5;
+    for (int i = 0; i < 64; ++i)
+      for (int jj = 0; jj < 64; ++jj) {
+        double s = i == jj ? 1.0 : 0.0;
+        for (int k = 0; k < 64; ++k) s += Bm[i * 64 + k] * Bm[jj * 64 + k] / 64.0;
+        h[(size_t)b * 4096 + jj * 64 + i] = s;
+      }
+  }
+  double *A, *L, *D;
+  CHK(hipMalloc(&A, h.size() * 8)); CHK(hipMalloc(&L, h.size() * 8)); CHK(hipMalloc(&D, h.size() * 8));
+  CHK(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+  auto run = [&](auto kern, const char* name) {
+    for (int B : {1, 256, 2048}) {
+      for (int w = 0; w < 5; ++w) hipLaunchKernelGGL(kern, dim3(B), dim3(64), 0, 0, A, L, D);
+      CHK(hipDeviceSynchronize());
+      const int reps = 50;
+      CHK(hipEventRecord(e0));
+      for (int k = 0; k < reps; ++k) hipLaunchKernelGGL(kern, dim3(B), dim3(64), 0, 0, A, L, D);
+      CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
+      float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+      printf("%-24s B=%5d  %8.2f us/launch\n", name, B, ms * 1e3 / reps);
+    }
+  };
+  run(kd<0>, "stage0 load+store");
+  run(kd<1>, "stage1 +potrf16");
+  run(kd<2>, "stage2 +diag inverses");
+  run(kd<3>, "stage3 +offdiag (full)");
+  run(kd<4>, "stage4 +epilogue");
+  // check: D * L = I for tile 0
+  std::vector<double> hl(4096), hd(4096);
+  CHK(hipMemcpy(hd.data(), D, 4096 * 8, hipMemcpyDeviceToHost));
+  hipLaunchKernelGGL(kd<1>, dim3(1), dim3(64), 0, 0, A, L, L);
+  CHK(hipMemcpy(hl.data(), L, 4096 * 8, hipMemcpyDeviceToHost));
+  // hl: rows in column-major? kd stores Dout[q*64 + r] = R[q] (row r) -> element (r, q) at q*64 + r
+  double err = 0;
+  for (int i = 0; i < 64; ++i)
+    for (int jj = 0; jj < 64; ++jj) {
+      double s = 0;
+      for (int k = 0; k < 64; ++k) s += hd[k * 64 + i] * hl[jj * 64 + k];
+      err = fmax(err, fabs(s - (i == jj)));
+    }
+  printf("max |Inv L - I| = %.3e\n", err);
+  return 0;
+}
