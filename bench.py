@@ -64,6 +64,7 @@ def parse():
                    help='day slices: equal-cost LPT mixes (lpt) or consecutive runs of the '
                         'largest-n-first order (ordered)')
     p.add_argument('--depth', type=int, default=3, help='slices in flight beyond the one waited on')
+    p.add_argument('--max-pool', type=int, default=0, help='max resident cells of the session (0: library default)')
     p.add_argument('--budget-s', type=float, default=420.0,
                    help='wall-clock budget from process start; stop submitting slices beyond it')
     p.add_argument('--nys-cells', type=int, default=0, help='nystrom workload: cells per rank-step')
@@ -657,7 +658,7 @@ def main():
         _lib.gpr_batch(prime.xyt, prime.z, prime.offs, prime.xs, prime.mean, x0=X0, opt=True, device=gpu,
                        profile=True)
     single = args.workload == 'single'
-    sess = None if single else _lib.Session(device=gpu, device_inputs=True, profile=True)
+    sess = None if single else _lib.Session(device=gpu, device_inputs=True, profile=True, max_pool=args.max_pool)
     if single:  # config 1: blocking one-shot calls (per-cell latency)
         for item in dev_warm:
             cells, xyt, z, h = item
