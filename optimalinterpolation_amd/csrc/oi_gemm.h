@@ -217,3 +217,95 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int nch, un
     __syncthreads();
   }
 }
+
+// ---- 128 x 128 variant: 512 threads, wave w owns rows 32*(w>>1) .. +32 and
+// columns 64*(w&1) .. +64 as 2 x 4 blocks of v_mfma_f64_16x16x4f64 (8
+// independent accumulators, 8 MFMAs per 6 LDS reads).  Each streamed tile
+// feeds two outputs: a 2 x 2 block of output tiles per workgroup, half the
+// operand traffic of the 64 x 128 core and a quarter of the 64 x 64 one
+// (tools/gemm4_probe.hip: 61 vs 52.5 / 35 TF/s streaming, 63 vs 59 / 53
+// L2-resident).  LDS: two buffers of (A, B) 16 x 128 chunks, row stride 144.
+#define GEMM4_LDSS 144
+#define GEMM4_STG (KC * GEMM4_LDSS)
+#define GEMM4_LDS (4 * GEMM4_STG)  // 9216 doubles = 72 KiB -> two workgroups per CU
+struct Quad8 {
+  d4 c[2][4];
+};
+__device__ __forceinline__ void quad8_zero(Quad8& q) {
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 4; ++b) q.c[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+}
+// coordinates in the 128 x 128 block of accumulator entry (mb, nb, r) of this lane
+__device__ __forceinline__ int acc4_row(int mb, int r) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  return 32 * (w >> 1) + 16 * mb + (lane >> 4) + 4 * r;
+}
+__device__ __forceinline__ int acc4_col(int nb) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  return 64 * (w & 1) + 16 * nb + (lane & 15);
+}
+
+// pair(p, a0, a1, b0, b1): the p-th operand tiles -- A for output rows 0..63 /
+// 64..127, B for output columns 0..63 / 64..127 (all k-major).  `nch` counts
+// 16-deep chunks (4 per pair; the last pair may be cut short).  MASKED: `skip`
+// (wave-uniform, bit 4*mb + nb) drops accumulator blocks whose outputs are
+// never used.
+template <bool MASKED, class PairFn>
+__device__ __forceinline__ void gemm4_kmajor(Quad8& acc, double* lds, int nch, unsigned skip, PairFn pair) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  if (nch <= 0) return;
+  if (MASKED) skip = __builtin_amdgcn_readfirstlane(skip);
+  const int sk = t >> 5, sm = (t & 31) * 2;  // this thread's 16 B of a 16 x 64 chunk
+  const int fr = lane & 15, fk = lane >> 4;
+  StageRegs r0, r1;  // a0 / a1 / b0 / b1: one 16 B piece of each operand tile
+  auto load = [&](int ch, StageRegs& q) __attribute__((always_inline)) {
+    const double *pa0, *pa1, *pb0, *pb1;
+    [[clang::always_inline]] pair(ch >> 2, pa0, pa1, pb0, pb1);
+    const int off = (ch & 3) * KC * GNB + t * 2;
+    q.a0 = gload2(pa0 + off);
+    q.a1 = gload2(pa1 + off);
+    q.b0 = gload2(pb0 + off);
+    q.b1 = gload2(pb1 + off);
+  };
+  auto store = [&](int buf, const StageRegs& q) __attribute__((always_inline)) {
+    double* As = lds + buf * 2 * GEMM4_STG;
+    double* Bs = As + GEMM4_STG;
+    *(dv2*)(As + sk * GEMM4_LDSS + sm) = q.a0;
+    *(dv2*)(As + sk * GEMM4_LDSS + 64 + sm) = q.a1;
+    *(dv2*)(Bs + sk * GEMM4_LDSS + sm) = q.b0;
+    *(dv2*)(Bs + sk * GEMM4_LDSS + 64 + sm) = q.b1;
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const double* As = lds + buf * 2 * GEMM4_STG;
+    const double* Bs = As + GEMM4_STG;
+#pragma unroll
+    for (int kk = 0; kk < KC / 4; ++kk) {
+      const int k = kk * 4 + fk;
+      const double a0 = As[k * GEMM4_LDSS + 32 * wr + fr];
+      const double a1 = As[k * GEMM4_LDSS + 32 * wr + 16 + fr];
+      double b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[q] = Bs[k * GEMM4_LDSS + 64 * wc + 16 * q + fr];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!MASKED || !(skip & (1u << q))) acc.c[0][q] = MFMA64(a0, b[q], acc.c[0][q]);
+        if (!MASKED || !(skip & (1u << (4 + q)))) acc.c[1][q] = MFMA64(a1, b[q], acc.c[1][q]);
+      }
+    }
+  };
+  load(0, r0);
+  load(min(1, nch - 1), r1);
+  store(0, r0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ch += 2) {
+    load(min(ch + 2, nch - 1), r0);
+    compute(0);
+    store(1, r1);
+    __syncthreads();
+    load(min(ch + 3, nch - 1), r1);
+    if (ch + 1 < nch) compute(1);
+    if (ch + 2 < nch) store(0, r0);
+    __syncthreads();
+  }
+}

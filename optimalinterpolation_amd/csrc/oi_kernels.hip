@@ -1076,6 +1076,132 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
   }
 }
 
+// ------------------------------------------------------ k_lauum_grad4 (default)
+// The same sums on 2 x 2 blocks of output tiles: workgroup (I2, J2), I2 >= J2,
+// covers tile rows i0 = 2 I2, i1 = i0 + 1 and columns j0 = 2 J2, j1 = j0 + 1
+// (512 threads, the 128 x 128 gemm4 core: every streamed W tile feeds two
+// outputs).  K^-1_{i,j} = sum_{k >= max(i, j)} W_ki^T W_kj: the block streams
+// k = i0 .. T-1 with W_{i0, i1} (k = i0) and W_{j0, j1} (k = j0 = i0 on a
+// diagonal block) the structural zero tile; k rows of the last tile beyond n
+// are skipped.  A wave's 32 x 64 accumulator lies in one output tile, so the
+// epilogue reduces per tile (two waves each, fixed order) and writes the
+// tile's partials at its usual slot.  Tiles beyond T, the block (i0, j1) of a
+// diagonal block and the upper triangles of diagonal tiles are masked out.
+__global__ __launch_bounds__(GEMM_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_lauum_grad4(const OiCell* __restrict__ cells,
+                                                             const int32_t* __restrict__ list,
+                                                             int gx, int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM4_LDS];
+  int ci, blk;
+  if (!xcd_cell_slot(gx, ncell, ci, blk)) return;
+  const OiCell& c = cells[list[ci]];
+  const int T = c.T, T2 = (T + 1) >> 1;
+  int I2, J2;
+  if (!decode_tri(blk, T2, I2, J2)) return;
+  if (*c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
+  const int i0 = 2 * I2, i1 = i0 + 1, j0 = 2 * J2, j1 = j0 + 1;
+  const int n = c.n, rT = n - NB * (T - 1);
+  const int nch = 4 * (T - i0 - 1) + (rT + KC - 1) / KC;
+  const int w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  // this wave's output tile and its 16x16 blocks that are never used
+  const int ti = wr >= 2 ? i1 : i0, tj = wc ? j1 : j0;
+  const bool tile_ok = ti < T && tj < T && ti >= tj;
+  unsigned skip = 0;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const int m0 = 32 * (wr & 1) + 16 * mb, n0 = 16 * nb;
+      const bool upper = ti == tj && m0 + 15 < n0;
+      const bool pad = (ti == T - 1 && m0 >= rT) || (tj == T - 1 && n0 >= rT);
+      if (!tile_ok || upper || pad) skip |= 1u << (4 * mb + nb);
+    }
+  const bool masked = I2 == J2 || i1 >= T - 1;  // diagonal block or the last block row
+  auto wpair = [=, &c](int p, const double*& a0, const double*& a1, const double*& b0, const double*& b1) {
+    const int k = i0 + p;
+    a0 = tileW(c, k, i0);
+    a1 = (i1 < T && k >= i1) ? tileW(c, k, i1) : g_zero_tile;
+    b0 = tileW(c, k, j0);
+    b1 = (j1 < T && k >= j1) ? tileW(c, k, j1) : g_zero_tile;
+  };
+  Quad8 acc;
+  quad8_zero(acc);
+  if (masked)
+    gemm4_kmajor<true>(acc, lds, nch, skip, wpair);
+  else
+    gemm4_kmajor<false>(acc, lds, nch, 0u, wpair);
+  // epilogue data: rows of tiles i0, i1 (entries 0..127), columns of j0, j1 (128..255)
+  double* uQ = lds;            // [3][256]
+  double* uq = lds + 3 * 256;  // [3][256]
+  double* al = lds + 6 * 256;  // [256]
+  double* dl = lds + 7 * 256;  // [256]
+  double* red = lds + 8 * 256; // [8 waves][5]
+  const int t = threadIdx.x;
+  __syncthreads();
+  if (t < 256) {
+    const int tt = t & 127;
+    const int a = t < 128 ? (tt < 64 ? i0 : i1) * NB + (tt & 63) : (tt < 64 ? j0 : j1) * NB + (tt & 63);
+    const bool in = a < n && (t < 128 ? (tt < 64 || i1 < T) : (tt < 64 || j1 < T));
+    for (int d = 0; d < 3; ++d) {
+      const double xv = in ? c.xyt[3 * a + d] : 0.0;
+      uQ[d * 256 + t] = (SQRT3 * xv) / c.hyp[d];
+      uq[d * 256 + t] = SQRT3 * (xv / c.hyp[d]);
+    }
+    al[t] = in ? c.vec[T * NB + a] : 0.0;
+    dl[t] = in ? c.dw[a] : 0.0;
+  }
+  __syncthreads();
+  const double sf2 = c.hyp[3];
+  double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (tile_ok) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int mr = acc4_row(mb, r), nc = acc4_col(nb);  // 0..127 within the block
+          const int m = mr & 63, nn = nc & 63;
+          const int a = ti * NB + m, b = tj * NB + nn;
+          if (a >= n || b >= n || (ti == tj && m < nn)) continue;
+          const double wgt = (a == b) ? 1.0 : 2.0;
+          const double w0 = acc.c[mb][nb][r] - al[mr] * al[128 + nc];  // (M^-1 - aa^T)_st
+          const double ww = (dl[mr] * dl[128 + nc]) * w0;               // (D M^-1 D - uu^T)_st
+          const double d0 = uQ[0 * 256 + mr] - uQ[0 * 256 + 128 + nc];
+          const double d1 = uQ[1 * 256 + mr] - uQ[1 * 256 + 128 + nc];
+          const double d2 = uQ[2 * 256 + mr] - uQ[2 * 256 + 128 + nc];
+          const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+          const double e = exp(-Q);
+          const double K = sf2 * ((1.0 + Q) * e);
+          const double q0 = uq[0 * 256 + mr] - uq[0 * 256 + 128 + nc];
+          const double q1 = uq[1 * 256 + mr] - uq[1 * 256 + 128 + nc];
+          const double q2 = uq[2 * 256 + mr] - uq[2 * 256 + 128 + nc];
+          s[0] += wgt * (ww * (sf2 * ((q0 * q0) * e)));
+          s[1] += wgt * (ww * (sf2 * ((q1 * q1) * e)));
+          s[2] += wgt * (ww * (sf2 * ((q2 * q2) * e)));
+          s[3] += wgt * (ww * (2.0 * K));
+          if (a == b) s[4] += w0;
+        }
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s[q] += __shfl_down(s[q], o, 64);
+  if ((t & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) red[w * 5 + q] = s[q];
+  __syncthreads();
+  if (t < 4) {  // tile slot t = (row half, column half); its waves are (2 rh) * 2 + ch and (2 rh + 1) * 2 + ch
+    const int rh = t >> 1, ch = t & 1;
+    const int ti2 = rh ? i1 : i0, tj2 = ch ? j1 : j0;
+    if (ti2 < T && tj2 < T && ti2 >= tj2) {
+      const int wa = (2 * rh) * 2 + ch, wb = (2 * rh + 1) * 2 + ch;
+      double* pp = c.part + OI_PART_GRAD(0) + 5 * ((size_t)ti2 * (ti2 + 1) / 2 + tj2);
+      for (int q = 0; q < 5; ++q) pp[q] = red[wa * 5 + q] + red[wb * 5 + q];
+    }
+  }
+}
+
 // ---------------------------------------------------------- k_finalize
 // nlZ = r.alpha/2 + sum log diag L + n log(2 pi)/2 (GPR:128); dnlZ (GPR:131-138)
 __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cells,
@@ -1343,9 +1469,19 @@ extern "C" int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncel
 extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                                     void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  const int gx = maxT * (maxT + 1) / 2;
-  hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,
-                     ncell);
+  static const int variant = [] {
+    const char* e = getenv("OI_LAUUM");
+    return e ? atoi(e) : 4;
+  }();
+  if (variant == 1) {  // one 64x64 tile per 256-thread workgroup (round 1 / A-B)
+    const int gx = maxT * (maxT + 1) / 2;
+    hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,
+                       ncell);
+  } else {
+    const int T2 = (maxT + 1) / 2, gx = T2 * (T2 + 1) / 2;
+    hipLaunchKernelGGL(k_lauum_grad4, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
+                       list, gx, ncell);
+  }
   return ret();
 }
 

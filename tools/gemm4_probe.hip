@@ -1,0 +1,133 @@
+// 128x128-output fp64 GEMM core (512 threads, each wave a 32x64 block of 2x4
+// v_mfma_f64_16x16x4f64) vs the 64x128 gemm2 core and the 64x64 gemm1 core.
+// D = sum_p A_p^T B_p over P k-major 64x64 tile pairs per output tile.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../optimalinterpolation_amd/csrc/oi_gemm.h"
+#define CHK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP error %s at %d\n",hipGetErrorString(e),__LINE__); exit(1);}}while(0)
+
+#define NTILES (1024 * 16 * 4)  // tiles allocated per operand array
+// tile address: mode 0 every WG streams its own tiles from HBM; mode 2 a few L2-resident tiles
+__device__ __forceinline__ const double* tile(const double* X, int mode, int wg, int P, int p, int which) {
+  size_t t = mode == 0 ? (((size_t)wg * P + p) * 4 + which) % NTILES : (size_t)((p + which) & 7);
+  return X + t * 4096;
+}
+
+struct Acc8 { d4 c[2][4]; };
+
+template <int LDSS>
+__global__ __launch_bounds__(512) void g4(const double* A, const double* B, double* C, int P, int mode) {
+  constexpr int STG = KC * LDSS;  // one 16 x 128 operand chunk
+  __shared__ __attribute__((aligned(16))) double lds[4 * STG];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  Acc8 acc;
+  for (int a = 0; a < 2; ++a) for (int b = 0; b < 4; ++b) acc.c[a][b] = (d4){0, 0, 0, 0};
+  const int nch = P * 4;
+  const int sk = t >> 5, sm = (t & 31) * 2;  // 16 B piece of a 16 x 64 chunk
+  struct Rg { dv2 a0, a1, b0, b1; };
+  Rg r0, r1;
+  auto load = [&](int ch, Rg& q) __attribute__((always_inline)) {
+    const int p = ch >> 2, off = (ch & 3) * KC * 64 + t * 2;
+    q.a0 = gload2(tile(A, mode, blockIdx.x, P, p, 0) + off);
+    q.a1 = gload2(tile(A, mode, blockIdx.x, P, p, 1) + off);
+    q.b0 = gload2(tile(B, mode, blockIdx.x, P, p, 2) + off);
+    q.b1 = gload2(tile(B, mode, blockIdx.x, P, p, 3) + off);
+  };
+  auto store = [&](int buf, const Rg& q) __attribute__((always_inline)) {
+    double* As = lds + buf * 2 * STG;
+    double* Bs = As + STG;
+    *(dv2*)(As + sk * LDSS + sm) = q.a0;
+    *(dv2*)(As + sk * LDSS + 64 + sm) = q.a1;
+    *(dv2*)(Bs + sk * LDSS + sm) = q.b0;
+    *(dv2*)(Bs + sk * LDSS + 64 + sm) = q.b1;
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const double* As = lds + buf * 2 * STG;
+    const double* Bs = As + STG;
+#pragma unroll
+    for (int kk = 0; kk < KC / 4; ++kk) {
+      const int k = kk * 4 + fk;
+      const double a0 = As[k * LDSS + 32 * wr + fr], a1 = As[k * LDSS + 32 * wr + 16 + fr];
+      double b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[q] = Bs[k * LDSS + 64 * wc + 16 * q + fr];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc.c[0][q] = MFMA64(a0, b[q], acc.c[0][q]);
+        acc.c[1][q] = MFMA64(a1, b[q], acc.c[1][q]);
+      }
+    }
+  };
+  load(0, r0);
+  load(1, r1);
+  store(0, r0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ch += 2) {
+    load(min(ch + 2, nch - 1), r0);
+    compute(0);
+    store(1, r1);
+    __syncthreads();
+    load(min(ch + 3, nch - 1), r1);
+    compute(1);
+    if (ch + 2 < nch) store(0, r0);
+    __syncthreads();
+  }
+  double s = 0;
+  for (int a = 0; a < 2; ++a) for (int b = 0; b < 4; ++b) for (int q = 0; q < 4; ++q) s += acc.c[a][b][q];
+  C[(size_t)blockIdx.x * 512 + t] = s;
+}
+
+__global__ __launch_bounds__(512) void g2(const double* A, const double* B, double* C, int P, int mode) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
+  Quad acc; quad_zero(acc);
+  const int wg = blockIdx.x;
+  gemm2_kmajor(acc, lds, P, [=](int p, const double*& a, const double*& b0, const double*& b1) {
+    a = tile(A, mode, wg, P, p, 0); b0 = tile(B, mode, wg, P, p, 2); b1 = tile(B, mode, wg, P, p, 3); });
+  double s = 0; for (int x = 0; x < 2; ++x) for (int y = 0; y < 2; ++y) for (int r = 0; r < 4; ++r) s += acc.c[x][y][r];
+  C[(size_t)wg * 512 + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void g1(const double* A, const double* B, double* C, int P, int mode) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
+  Quad acc; quad_zero(acc);
+  const int wg = blockIdx.x;
+  gemm1_kmajor<false>(acc, lds, 4 * P, 0u, [=](int p, const double*& a, const double*& b) {
+    a = tile(A, mode, wg, P, p, 0); b = tile(B, mode, wg, P, p, 2); });
+  double s = 0; for (int x = 0; x < 2; ++x) for (int y = 0; y < 2; ++y) for (int r = 0; r < 4; ++r) s += acc.c[x][y][r];
+  C[(size_t)wg * 512 + threadIdx.x] = s;
+}
+
+__global__ void fill(double* X, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) X[i] = 1.0 + 1e-3 * (double)(i % 97);
+}
+
+int main() {
+  const int P = 16, nwg = 1024;
+  size_t tiles_n = NTILES;
+  double *A, *B, *C;
+  CHK(hipMalloc(&A, tiles_n * 4096 * 8)); CHK(hipMalloc(&B, tiles_n * 4096 * 8)); CHK(hipMalloc(&C, (size_t)nwg * 4 * 512 * 8));
+  const size_t nel = tiles_n * 4096;
+  hipLaunchKernelGGL(fill, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, 0, A, nel);
+  hipLaunchKernelGGL(fill, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, 0, B, nel);
+  CHK(hipDeviceSynchronize());
+  hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+  auto run = [&](const char* name, auto kern, int threads, int nwgs, double flop_per_wg) {
+    for (int mode : {0, 2}) {
+      hipLaunchKernelGGL(kern, dim3(nwgs), dim3(threads), 0, 0, A, B, C, P, mode); CHK(hipDeviceSynchronize());
+      CHK(hipEventRecord(e0));
+      for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(kern, dim3(nwgs), dim3(threads), 0, 0, A, B, C, P, mode);
+      CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
+      float ms; CHK(hipEventElapsedTime(&ms, e0, e1)); ms /= 5;
+      printf("%-16s %-7s %8.3f ms %6.2f TF/s\n", name, mode == 0 ? "stream" : "L2res", ms, flop_per_wg * nwgs / ms / 1e9);
+    }
+  };
+  const double tp = 2.0 * 64 * 64 * 64 * P;  // one output tile
+  run("g1 64x64", g1, 256, 4 * nwg, tp);
+  run("g2 64x128", g2, 512, 2 * nwg, 2 * tp);
+  run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
+  run("g4 128x128 s136", g4<136>, 512, nwg, 4 * tp);
+  return 0;
+}
