@@ -63,8 +63,7 @@ struct OiCell {
 
 // partial-sum layout inside OiCell::part (ntile = T(T+1)/2)
 #define OI_PART_GRAD(ntile) 0              // 5 per tile: s0 s1 s2 sK2 trace
-#define OI_PART_QUAD(ntile) (5 * (ntile))  // T: r_k . alpha_k
-#define OI_PART_LOGDET(ntile, T) (5 * (ntile) + (T))  // T: sum log diag(L_kk)
+#define OI_PART_LOGDET(ntile, T) (5 * (ntile) + (T))  // T: sum log diag(L_kk) (T slots before it spare)
 #define OI_PART_PRED(ntile, T) (5 * (ntile) + 2 * (T))  // 3 per block: z.z, z.v, v.v
 #define OI_PART_SIZE(ntile, T) (5 * (ntile) + 5 * (T))
 
@@ -86,7 +85,6 @@ int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, in
                          int kbeg, int with_trtri, void* stream);
 int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
                          int with_trtri, void* stream);
-int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                          void* stream);
 int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, void* stream);

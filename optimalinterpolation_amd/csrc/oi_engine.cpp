@@ -117,10 +117,9 @@ size_t cell_bytes(int64_t n, bool eval) {
 }
 
 // ------------------------------------------------------------- profiling
-enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_EVEN, K_ZVEC, K_AVEC, K_LAUUM, K_FINAL, K_PRED, K_COUNT };
+enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_EVEN, K_LAUUM, K_FINAL, K_COUNT };
 const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_chol_panel",
-                                    "k_panel_even", "k_zvec", "k_avec", "k_lauum_grad",
-                                    "k_finalize", "k_predict"};
+                                    "k_panel_even", "k_lauum_grad", "k_finalize"};
 
 // Panel scheme, read per call from OI_PANEL:
 //   2 (default): even/odd block-column pairs share one stream (k_panel_even +
@@ -718,10 +717,8 @@ class Engine {
     }
     cur_j = -1;
     cur_cells = ne;
-    // z = L^-1 r was built during the factorisation (k_diag_factor / panels)
-    mark(K_AVEC, false);
-    rc |= oi_launch_avec(dc, dl_ev, ne, maxTe, gst);
-    mark(K_AVEC, true);
+    // z = L^-1 r and alpha = W^T z were built during the factorisation
+    // (k_diag_factor and the panels), quad = z^T z
     mark(K_LAUUM, false);
     rc |= oi_launch_lauum_grad(dc, dl_ev, ne, maxTe, gst);
     mark(K_LAUUM, true);

@@ -17,8 +17,9 @@
 //                  products per tile, look-ahead of tile j+1       (both) 2 n^3/3
 //                  (kbeg = 0: the one-column scheme, OI_PANEL=1)
 //   (forward substitution z = L^-1 r runs inside the factorisation: k_diag_factor
-//                  applies Dinv_jj to block j, the panels subtract L_ij z_j)
-//   k_avec         alpha = W^T z  (alpha = K^-1 r, GPR:127)                   O(n^2)
+//                  applies Dinv_jj to block j, the panels subtract L_ij z_j; and
+//                  alpha = W^T z = K^-1 r (GPR:127) is accumulated as each W tile
+//                  is finished: alpha_jj += W_j,jj^T z_j; r^T alpha = z^T z)
 //   k_lauum_grad1  K^-1 = W^T W, one tile per workgroup, fused with the
 //                  gradient traces sum((K^-1 - alpha alpha^T) o dK_j); K and
 //                  dK_j are regenerated from coordinates (GPR:130-138)         n^3/3
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
   for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
   // forward substitution, block j: z_j = Dinv_jj (r_j - sum_{k<j} L_jk z_k) -- the
   // panels already subtracted the sum -- and v_j likewise for predict (k* rhs)
+  double zn = 0.0;
   {
     const bool pred = c.mode == OI_MODE_PREDICT;
     double* zj = c.vec + j * NB;
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
     Tt[r] = zj[r];
     Tt[NB + r] = pred ? vj[r] : 0.0;
     __syncthreads();
-    double zn = 0.0, vn = 0.0;
+    double vn = 0.0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       zn = fma(R[q], Tt[q], zn);
@@ -379,8 +381,16 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
 #pragma unroll
     for (int q = 0; q < NB; ++q) Tt[q * 65 + r] = R[q];  // Tt[c][r] = Inv[r][c]
     __syncthreads();
+    Tt[NB * 65 + r] = zn;
+    __syncthreads();
     double* Wj = tileW(c, j, j);
-    for (int q = 0; q < NB; ++q) Wj[q * NB + r] = Tt[r * 65 + q];  // W[q][r], row-major
+    double al = 0.0;  // alpha_j = W_jj^T z_j starts the alpha = W^T z accumulation
+    for (int q = 0; q < NB; ++q) {
+      const double wv = Tt[r * 65 + q];
+      Wj[q * NB + r] = wv;  // W[q][r], row-major
+      al = fma(wv, Tt[NB * 65 + q], al);
+    }
+    c.vec[c.T * NB + j * NB + r] = al;
   }
 }
 
@@ -546,6 +556,7 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
 #pragma unroll
   for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
   // forward substitution, block j (see k_diag_factor)
+  double zn = 0.0;
   {
     const bool pred = c.mode == OI_MODE_PREDICT;
     double* zj = c.vec + j * NB;
@@ -553,7 +564,7 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     Xs[r] = zj[r];
     Xs[NB + r] = pred ? vj[r] : 0.0;  // Xs has room for 272 doubles
     __syncthreads();
-    double zn = 0.0, vn = 0.0;
+    double vn = 0.0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       zn = fma(R[q], Xs[q], zn);
@@ -579,8 +590,15 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < NB; ++q) lds16[q * D16_LD + r] = R[q];  // lds16[c*65 + r] = Inv[r][c]
+    Xs[2 * NB + r] = zn;
     __syncthreads();
-    for (int q = 0; q < NB; ++q) Wj[q * NB + r] = lds16[r * D16_LD + q];
+    double al = 0.0;  // alpha_j = W_jj^T z_j starts the alpha = W^T z accumulation
+    for (int q = 0; q < NB; ++q) {
+      const double wv = lds16[r * D16_LD + q];
+      Wj[q * NB + r] = wv;
+      al = fma(wv, Xs[2 * NB + q], al);
+    }
+    c.vec[c.T * NB + j * NB + r] = al;
   }
 }
 
@@ -710,6 +728,42 @@ __device__ __forceinline__ void fwd_update(const OiCell& c, const double* X, int
   }
 }
 
+// alpha = W^T z accumulated while W is built (round 2; replaces k_avec):
+// once tile W_{j,jj} is final, alpha_jj += W_{j,jj}^T z_j (z_j final since
+// k_diag_factor(j), which also starts alpha_j = W_jj^T z_j).  Same staging as
+// fwd_update: the tile sits in LDS as X[col * ld + row] with the product's
+// output index as `row`; thread t < 64 preloads alpha_jj[t], 64..127 z_j.
+__device__ __forceinline__ double alpha_preload(const OiCell& c, int jj, int j) {
+  const int t = threadIdx.x;
+  if (t < 64) return c.vec[c.T * NB + jj * NB + t];
+  if (t < 128) return c.vec[j * NB + t - 64];
+  return 0.0;
+}
+
+template <int NTHREADS>
+__device__ __forceinline__ void alpha_update(const OiCell& c, const double* X, int ld, int jj, double pre,
+                                             double* scratch) {
+  constexpr int G = NTHREADS / 64, CW = NB / G;
+  const int t = threadIdx.x, row = t & 63, grp = t >> 6;
+  double* red = scratch;
+  double* zj = scratch + G * NB;
+  if (t >= 64 && t < 128) zj[t - 64] = pre;
+  __syncthreads();
+  double sa = 0.0;
+#pragma unroll 4
+  for (int q = 0; q < CW; ++q) {
+    const int col = grp * CW + q;
+    sa = fma(X[col * ld + row], zj[col], sa);
+  }
+  red[grp * NB + row] = sa;
+  __syncthreads();
+  if (t < 64) {
+    double a = 0.0;
+    for (int g = 0; g < G; ++g) a += red[g * NB + row];
+    c.vec[c.T * NB + jj * NB + row] = pre + a;
+  }
+}
+
 // --------------------------------------------------- k_chol_panel(j)
 // One 256-thread workgroup per output tile; logical slots of a cell:
 //   x <  T-1-j : tile (i = j+1+x, j) of the factor, one GEMM loop:
@@ -808,6 +862,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
     a = k < j ? Pj + (size_t)k * OI_TILE : Dj;
     b = tileW(c, k, jj);  // k == j: Vneg
   };
+  const double apre = alpha_preload(c, jj, j);
   if (j == T - 1 && rT < NB)  // m = row of W block row j
     gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst + extra), pad_skip(32 * wr, 32 * wc, rT, NB), wpair);
   else
@@ -815,8 +870,12 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   double* Wt = tileW(c, j, jj);
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r) {
         Wt[acc1_row(mb, r) * NB + acc1_col(nb)] = acc.c[mb][nb][r];  // row-major
+        lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // X[row of W * XLD + col]
+      }
+  __syncthreads();
+  alpha_update<256>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
 }
 
 // --------------------------------------------------- k_panel_even(j), j even
@@ -940,47 +999,14 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   };
   // n = row of W block row j (half 0) or j+1 (half 1)
   const int nlim = ((wc < 2 && j == T - 1) || (wc >= 2 && j + 1 == T - 1)) ? rT : NB;
+  const double apre = alpha_preload(c, jj, j);
   if (nlim < NB)
     gemm2_kmajor<true>(acc, lds, j - jj, wpair, pad_skip(0, 32 * (wc & 1), NB, nlim));
   else
     gemm2_kmajor<false>(acc, lds, j - jj, wpair);
-  emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);           // W_j,jj (row-major)
+  emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);           // W_j,jj (row-major), staged X[n*XLD+m]
+  alpha_update<GEMM_THREADS>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
   if (has_next) emit_half(acc, 1, lds, tileW(c, j + 1, jj), EMIT_NEG);  // Vneg
-}
-
-// ------------------------------------------------------------- k_avec
-// alpha_k = sum_{i>=k} W_ik^T z_i ; partial r_k . alpha_k
-__global__ __launch_bounds__(256) void k_avec(const OiCell* __restrict__ cells,
-                                              const int32_t* __restrict__ list, int gx,
-                                              int ncell) {
-  int ci, k;
-  if (!xcd_cell_slot(gx, ncell, ci, k)) return;
-  const OiCell& c = cells[list[ci]];
-  const int T = c.T;
-  if (k >= T || *c.status != OI_OK || c.mode != OI_MODE_EVAL) return;
-  __shared__ double red[4][NB + 1];
-  const int t = threadIdx.x, cc = t & 63, mq = t >> 6, n = c.n;
-  const double* z = c.vec;
-  double s = 0.0;
-  for (int i = k; i < T; ++i) {
-    const double* Wt = tileW(c, i, k);
-#pragma unroll 4
-    for (int mm = 0; mm < 16; ++mm) {
-      const int m = 16 * mq + mm;
-      s += Wt[m * NB + cc] * z[i * NB + m];
-    }
-  }
-  red[mq][cc] = s;
-  __syncthreads();
-  if (t < NB) {
-    const double a = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-    double* alpha = c.vec + T * NB;
-    alpha[k * NB + t] = a;
-    const int b = k * NB + t;
-    double p = b < n ? c.r[b] * a : 0.0;
-    for (int o = 32; o >= 1; o >>= 1) p += __shfl_down(p, o, 64);
-    if (t == 0) c.part[OI_PART_QUAD(T * (T + 1) / 2) + k] = p;
-  }
 }
 
 // ------------------------------------------------------ k_lauum_grad
@@ -1076,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
   }
 }
 
-// ------------------------------------------------------ k_lauum_grad4 (default)
+// ------------------------------------------------------ k_lauum_grad4 (OI_LAUUM=4)
 // The same sums on 2 x 2 blocks of output tiles: workgroup (I2, J2), I2 >= J2,
 // covers tile rows i0 = 2 I2, i1 = i0 + 1 and columns j0 = 2 J2, j1 = j0 + 1
 // (512 threads, the 128 x 128 gemm4 core: every streamed W tile feeds two
@@ -1242,7 +1268,7 @@ __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cel
   for (int x = t; x < nslot; x += 256)
     for (int q = 0; q < 5; ++q) v[q] += c.part[OI_PART_GRAD(ntile) + 5 * x + q];
   for (int k = t; k < T; k += 256) {
-    v[5] += c.part[OI_PART_QUAD(ntile) + k];
+    v[5] += c.part[OI_PART_PRED(ntile, T) + 3 * k];  // r^T alpha = z^T z, z = L^-1 r
     v[6] += c.part[OI_PART_LOGDET(ntile, T) + k];
   }
   block_sum<7, 4>(v, red);
@@ -1458,22 +1484,14 @@ extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, in
   return ret();
 }
 
-extern "C" int oi_launch_avec(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                              void* stream) {
-  if (ncell <= 0 || maxT <= 0) return 0;
-  hipLaunchKernelGGL(k_avec, dim3(grid1(maxT, ncell)), dim3(256), 0, S(stream), cells, list, maxT,
-                     ncell);
-  return ret();
-}
-
 extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                                     void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
   static const int variant = [] {
     const char* e = getenv("OI_LAUUM");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 1;
   }();
-  if (variant == 1) {  // one 64x64 tile per 256-thread workgroup (round 1 / A-B)
+  if (variant != 4) {  // one 64x64 tile per 256-thread workgroup (default: measured faster)
     const int gx = maxT * (maxT + 1) / 2;
     hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,
                        ncell);
