@@ -71,6 +71,7 @@ struct OiCell {
 //   eval   : [0] nlZ, [1..6] dnlZ
 //   predict: [0] fs, [1] sd, [2] lZ
 #define OI_OUT_N 8
+#define OI_OUT_STATUS 7  // the cell's status after the round (k_finalize), as a double
 
 #ifdef __cplusplus
 extern "C" {

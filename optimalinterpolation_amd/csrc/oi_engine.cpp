@@ -338,18 +338,15 @@ class Engine {
     if (const char* eg = getenv("OI_GROUPS")) G_ = std::max(1, std::min(8, atoi(eg)));
     if (cap_ < 2 * G_) G_ = 1;
     capG_ = (cap_ + G_ - 1) / G_;
-    d_cells_.reserve(cap_ * sizeof(OiCell));
-    h_cells_.reserve(cap_ * sizeof(OiCell));
-    d_list_.reserve((size_t)G_ * capG_ * 4 * 3);
-    h_list_.reserve((size_t)G_ * capG_ * 4 * 3);
+    // one block per group, mirrored on the host, so a round uploads its cell
+    // records, lists and cleared status words in ONE copy (and the status comes
+    // back inside the result rows, OI_OUT_STATUS): two copies per round, not five
+    blk_ = ((size_t)capG_ * (sizeof(OiCell) + 4 * 3 + 4) + 255) & ~size_t(255);
+    d_blk_.reserve(G_ * blk_);
+    h_blk_.reserve(G_ * blk_);
     d_res_.reserve(cap_ * OI_OUT_N * 8);
     h_res_.reserve(cap_ * OI_OUT_N * 8);
-    d_stat_.reserve(cap_ * 4);
-    h_stat_.reserve(cap_ * 4);
-    hc_ = (OiCell*)h_cells_.p;
-    dc_ = (const OiCell*)d_cells_.p;
     hres_ = (double*)h_res_.p;
-    hst_ = (int32_t*)h_stat_.p;
     groups_.resize(G_);
     for (int g = 0; g < G_; ++g) {
       Group& gr = groups_[g];
@@ -357,8 +354,14 @@ class Engine {
       gr.cap = std::max(0, std::min(capG_, cap_ - g * capG_));
       gr.st = g == 0 ? st_ : ctx.aux_stream(g);
       for (int s = gr.s0 + gr.cap - 1; s >= gr.s0; --s) gr.free_slots.push_back(s);
-      gr.hl = (int32_t*)h_list_.p + (size_t)g * capG_ * 3;
-      gr.dl = (int32_t*)d_list_.p + (size_t)g * capG_ * 3;
+      char* hb = (char*)h_blk_.p + g * blk_;
+      char* db = (char*)d_blk_.p + g * blk_;
+      gr.hc = (OiCell*)hb;
+      gr.dc = (OiCell*)db;
+      gr.hl = (int32_t*)(hb + capG_ * sizeof(OiCell));
+      gr.dl = (int32_t*)(db + capG_ * sizeof(OiCell));
+      gr.hstat = gr.hl + 3 * capG_;
+      gr.dstat = gr.dl + 3 * capG_;
       if (o.profile) {
         gr.ev.resize(2 * (3 * 1024 + 16));
         for (auto& ee : gr.ev) HIPC(hipEventCreate(&ee));
@@ -522,14 +525,23 @@ class Engine {
     int s0 = 0, cap = 0;
     hipStream_t st = nullptr;
     std::vector<int> free_slots, active, ev_slots, pr_slots;
-    int32_t* hl = nullptr;  // host lists: all | eval | predict (capG each)
+    OiCell* hc = nullptr;   // cell records of the group's slots (host mirror / device)
+    OiCell* dc = nullptr;
+    int32_t* hl = nullptr;  // lists all | eval | predict (capG each), group-local slot indices
     int32_t* dl = nullptr;
+    int32_t* hstat = nullptr;  // status words (cleared on the host every round)
+    int32_t* dstat = nullptr;
     bool inflight = false;
     int maxT = 0;
     std::vector<hipEvent_t> ev;
     std::vector<int> ev_kind;
     std::vector<std::pair<int, int>> ev_meta;
   };
+
+  OiCell& hcell(int s) {
+    Group& gr = groups_[s / capG_];
+    return gr.hc[s - gr.s0];
+  }
 
   void release_job(Job* jp) {
     if (jp->in_off != SIZE_MAX) ctx_.arena.release(jp->in_off, jp->in_bytes);
@@ -559,7 +571,7 @@ class Engine {
       sl.bytes = bytes;
       if (poison_)  // debug: NaN-fill the cell's workspace so any read-before-write shows
         HIPC(hipMemsetAsync(ctx_.arena.ptr(off), 0xFF, bytes, gr.st));
-      OiCell& cd = hc_[s];
+      OiCell& cd = hcell(s);
       std::memset(&cd, 0, sizeof(cd));
       const int T = tiles_of(n);
       const size_t nt = (size_t)T * (T + 1) / 2;
@@ -579,7 +591,7 @@ class Engine {
       cd.r = job.v + job.offs[c];
       cd.dw = job.dw + job.offs[c];
       cd.out = (double*)d_res_.p + (size_t)s * OI_OUT_N;
-      cd.status = (int32_t*)d_stat_.p + s;
+      cd.status = gr.dstat + (s - gr.s0);
       cd.n = (int32_t)n;
       cd.n_obs = (int32_t)(job.offs[c + 1] - job.offs[c]);
       cd.ssw = job.ssw[c];
@@ -606,12 +618,12 @@ class Engine {
 
   void launch_round(Group& gr) {
     hipStream_t gst = gr.st;
-    OiCell* hc = hc_;
+    auto hc = [&](int s) -> OiCell& { return gr.hc[s - gr.s0]; };
     gr.ev_slots.clear();
     gr.pr_slots.clear();
     for (int s : gr.active) {
       Slot& sl = slots_[s];
-      OiCell& cd = hc[s];
+      OiCell& cd = hc(s);
       if (sl.phase == 0) {
         for (int k = 0; k < 5; ++k) cd.hyp[k] = std::exp(sl.mail.x[k]);  // GPR:120-122
         cd.mode = OI_MODE_EVAL;
@@ -627,33 +639,31 @@ class Engine {
       }
     }
     auto byT = [&](std::vector<int>& v) {
-      std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return hc[a].T > hc[b].T; });
+      std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return hc(a).T > hc(b).T; });
     };
     byT(gr.ev_slots);
     byT(gr.pr_slots);
     std::vector<int> all_slots;
     all_slots.reserve(gr.active.size());
     std::merge(gr.ev_slots.begin(), gr.ev_slots.end(), gr.pr_slots.begin(), gr.pr_slots.end(),
-               std::back_inserter(all_slots), [&](int a, int b) { return hc[a].T > hc[b].T; });
+               std::back_inserter(all_slots), [&](int a, int b) { return hc(a).T > hc(b).T; });
     const int na = (int)all_slots.size(), ne = (int)gr.ev_slots.size(),
               np_ = (int)gr.pr_slots.size();
     int32_t* l_all = gr.hl;
     int32_t* l_ev = gr.hl + capG_;
     int32_t* l_pr = gr.hl + 2 * capG_;
-    for (int k = 0; k < na; ++k) l_all[k] = all_slots[k];
-    for (int k = 0; k < ne; ++k) l_ev[k] = gr.ev_slots[k];
-    for (int k = 0; k < np_; ++k) l_pr[k] = gr.pr_slots[k];
-    const int maxT = na ? hc[all_slots[0]].T : 0;
-    const int maxTe = ne ? hc[gr.ev_slots[0]].T : 0;
+    for (int k = 0; k < na; ++k) l_all[k] = all_slots[k] - gr.s0;
+    for (int k = 0; k < ne; ++k) l_ev[k] = gr.ev_slots[k] - gr.s0;
+    for (int k = 0; k < np_; ++k) l_pr[k] = gr.pr_slots[k] - gr.s0;
+    const int maxT = na ? hc(all_slots[0]).T : 0;
+    const int maxTe = ne ? hc(gr.ev_slots[0]).T : 0;
     gr.maxT = maxT;
 
-    HIPC(hipMemcpyAsync((OiCell*)d_cells_.p + gr.s0, hc + gr.s0, gr.cap * sizeof(OiCell),
-                        hipMemcpyHostToDevice, gst));
-    HIPC(hipMemcpyAsync(gr.dl, gr.hl, (size_t)capG_ * 4 * 3, hipMemcpyHostToDevice, gst));
-    HIPC(hipMemsetAsync((int32_t*)d_stat_.p + gr.s0, 0, gr.cap * 4, gst));
+    std::memset(gr.hstat, 0, (size_t)capG_ * 4);
+    HIPC(hipMemcpyAsync(gr.dc, gr.hc, blk_, hipMemcpyHostToDevice, gst));
     const int32_t* dl_all = gr.dl;
     const int32_t* dl_ev = gr.dl + capG_;
-    const OiCell* dc = dc_;
+    const OiCell* dc = gr.dc;
 
     gr.ev_kind.clear();
     gr.ev_meta.clear();
@@ -675,7 +685,7 @@ class Engine {
     mark(K_BUILD, true);
     for (int j = 0; j < maxT; ++j) {
       int cnt = 0;
-      while (cnt < na && hc[all_slots[cnt]].T > j) ++cnt;
+      while (cnt < na && hc(all_slots[cnt]).T > j) ++cnt;
       cur_j = j;
       cur_cells = cnt;
       mark(K_CHOL, false);
@@ -697,7 +707,7 @@ class Engine {
       }
       if (o_.profile) {  // executed MFMA flops: 2*64^3 per 64x64 tile product
         for (int k = 0; k < cnt; ++k) {
-          const OiCell& cd = hc[all_slots[k]];
+          const OiCell& cd = hc(all_slots[k]);
           const bool ev = cd.mode == OI_MODE_EVAL;
           kfl_[K_SCALE] += tf * (double)(j - kbeg);
           if (even) {  // 64x128 blocks: two products per streamed pair
@@ -730,11 +740,9 @@ class Engine {
     if (rc) throw HipError(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     HIPC(hipMemcpyAsync(hres_ + (size_t)gr.s0 * OI_OUT_N, (double*)d_res_.p + (size_t)gr.s0 * OI_OUT_N,
                         (size_t)gr.cap * OI_OUT_N * 8, hipMemcpyDeviceToHost, gst));
-    HIPC(hipMemcpyAsync(hst_ + gr.s0, (int32_t*)d_stat_.p + gr.s0, (size_t)gr.cap * 4,
-                        hipMemcpyDeviceToHost, gst));
     if (o_.profile) {
       for (int k = 0; k < ne; ++k) {
-        const OiCell& cd = hc[gr.ev_slots[k]];
+        const OiCell& cd = hc(gr.ev_slots[k]);
         for (int i = 0; i < cd.T; ++i) kfl_[K_LAUUM] += tf * (double)(cd.T - i) * (i + 1);
       }
     }
@@ -758,7 +766,7 @@ class Engine {
       }
       double rms = 0.0, work = 0.0;
       for (const auto& rr : recs) rms += rr.ms;
-      for (int s : gr.ev_slots) work += std::pow((double)hc_[s].T, 3.0);
+      for (int s : gr.ev_slots) work += std::pow((double)hcell(s).T, 3.0);
       std::lock_guard<std::mutex> pl(g_prof_mu);
       g_last_round.swap(recs);
       g_rounds.push_back({(int)gr.ev_slots.size(), (int)gr.pr_slots.size(), gr.maxT, work, rms});
@@ -769,6 +777,7 @@ class Engine {
       Slot& sl = slots_[s];
       Job& job = *sl.job;
       const double* rr = hres_ + (size_t)s * OI_OUT_N;
+      const int32_t st = (int32_t)rr[OI_OUT_STATUS];
       const int64_t c = sl.cell;
       bool done = false;
       if (sl.phase == 0) {
@@ -786,7 +795,7 @@ class Engine {
         ++evals_;
         job.nlz[c] = rr[0];
         for (int k = 0; k < oi::NH; ++k) job.grad[6 * c + k] = rr[1 + k];
-        if (job.status) job.status[c] = hst_[s];
+        if (job.status) job.status[c] = st;
         done = true;
       } else {
         ++predicts_;
@@ -795,10 +804,10 @@ class Engine {
         dst[1] = rr[1];
         dst[2] = rr[2];
         for (int k = 0; k < 5; ++k) dst[3 + k] = sl.hyp[k];
-        if (hst_[s] != OI_OK) {
+        if (st != OI_OK) {
           for (int k = 0; k < 8; ++k) dst[k] = NAN;  // GPR:187-189
         }
-        if (job.status) job.status[c] = hst_[s];
+        if (job.status) job.status[c] = st;
         if (job.info) {
           int32_t* inf = job.info + 4 * c;
           inf[0] = sl.res.nit;
@@ -850,12 +859,10 @@ class Engine {
   int cap_ = 1, G_ = 1, capG_ = 1;
   std::vector<Slot> slots_;
   std::vector<Group> groups_;
-  DBuf d_cells_, d_list_, d_res_, d_stat_;
-  HBuf h_cells_, h_list_, h_res_, h_stat_;
-  OiCell* hc_ = nullptr;
-  const OiCell* dc_ = nullptr;
+  DBuf d_blk_, d_res_;
+  HBuf h_blk_, h_res_;
+  size_t blk_ = 0;  // bytes of one group's round block
   double* hres_ = nullptr;
-  int32_t* hst_ = nullptr;
   std::deque<std::pair<Job*, int64_t>> queue_;
   std::map<int64_t, std::unique_ptr<Job>> jobs_;
   int64_t next_id_ = 0;
@@ -1107,9 +1114,11 @@ int64_t oi_profile_json(char* buf, int64_t len) {
     s += tmp;
   }
   char tmp[256];
-  std::snprintf(tmp, sizeof(tmp), "},\"rounds\":%lld,\"evals\":%lld,\"predicts\":%lld,\"wall_s\":%.6f",
+  std::snprintf(tmp, sizeof(tmp),
+                "},\"rounds\":%lld,\"evals\":%lld,\"predicts\":%lld,\"wall_s\":%.6f,\"sync_s\":%.6f,"
+                "\"setup_s\":%.6f",
                 (long long)g_run.rounds, (long long)g_run.evals, (long long)g_run.predicts,
-                g_run.wall_s);
+                g_run.wall_s, g_run.sync_s, g_run.setup_s);
   s += tmp;
   s += ",\"last_round\":[";
   for (size_t q = 0; q < g_last_round.size(); ++q) {

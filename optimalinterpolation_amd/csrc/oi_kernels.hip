@@ -54,6 +54,13 @@ extern "C" int oi_set_debug(int on) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_debug), &on, sizeof(int)) == hipSuccess ? 0 : -1;
 }
 
+// Descriptor pointers are generic, so plain accesses through them compile to
+// flat_* instructions, which count against lgkmcnt as well: every LDS wait and
+// single-wave barrier then also waits for the tile stores still in flight.
+// gst / gld access through the global address space (global_* instructions).
+typedef __attribute__((address_space(1))) double gdouble;
+__device__ __forceinline__ void gst(double* p, double v) { *(gdouble*)p = v; }
+__device__ __forceinline__ double gld(const double* p) { return *(const gdouble*)p; }
 __device__ __forceinline__ size_t tri(int i) { return (size_t)i * (i + 1) / 2; }
 __device__ __forceinline__ double* tileL(const OiCell& c, int i, int j) {
   return c.L + (tri(i) + j) * OI_TILE;
@@ -158,7 +165,7 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
     // factorisation: z = r (site residuals), and for predict v = k* = D kd*
     // (GPR:174, cdist of scaled coordinates)
     const int a = i * NB + t;
-    c.vec[a] = a < n ? c.r[a] : 0.0;
+    gst(c.vec + a, a < n ? c.r[a] : 0.0);
     if (c.mode == OI_MODE_PREDICT) {
       double kv = 0.0;
       if (a < n) {
@@ -170,7 +177,7 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
         const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
         kv = c.dw[a] * (sf2 * ((1.0 + Q) * exp(-Q)));
       }
-      c.vec[3 * c.T * NB + a] = kv;
+      gst(c.vec + 3 * c.T * NB + a, kv);
     }
   }
   double* Y = tileL(c, i, j);
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
       val = (dws[0][r] * dws[1][cc]) * (sf2 * ((1.0 + Q) * exp(-Q)));  // M = D Kd D (+ sn2 I)
       if (a == b) val += sn2;
     }
-    Y[e] = val;
+    gst(Y + e, val);
   }
 }
 
@@ -249,7 +256,7 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
   double* Y = tileL(c, j, j);
   double R[NB];
 #pragma unroll
-  for (int q = 0; q < NB; ++q) R[q] = Y[q * NB + r];  // row r of the column-major tile
+  for (int q = 0; q < NB; ++q) R[q] = gld(Y + q * NB + r);  // row r of the column-major tile
   double* S0 = Tt;             // 32 x 33
   double* S1 = Tt + 32 * 33;   // 32 x 33
   double* S2 = Tt + 64 * 33;   // 32 x 33
@@ -295,13 +302,14 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
     }
     return;
   }
-  double lg = 0.0;
+  double dg = 1.0;  // L_rr, picked out by selects: one log per lane, not one per q
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
-    if (q > r) R[q] = 0.0;                                   // clear the upper part
-    if (q == r) lg = (j * NB + r < c.n) ? log(R[q]) : 0.0;   // log L_rr
-    Y[q * NB + r] = R[q];                                    // L_jj, column-major
+    if (q > r) R[q] = 0.0;  // clear the upper part
+    dg = q == r ? R[q] : dg;
+    gst(Y + q * NB + r, R[q]);  // L_jj, column-major
   }
+  double lg = (j * NB + r < c.n) ? log(dg) : 0.0;  // log L_rr
   for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
   if (r == 0) {
     const int ntile = c.T * (c.T + 1) / 2;
@@ -344,7 +352,7 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
   __syncthreads();  // Tt is reused below
   double* Dj = tileD(c, j);
 #pragma unroll
-  for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
+  for (int q = 0; q < NB; ++q) gst(Dj + q * NB + r, R[q]);  // column-major
   // forward substitution, block j: z_j = Dinv_jj (r_j - sum_{k<j} L_jk z_k) -- the
   // panels already subtracted the sum -- and v_j likewise for predict (k* rhs)
   double zn = 0.0;
@@ -361,8 +369,8 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
       zn = fma(R[q], Tt[q], zn);
       vn = fma(R[q], Tt[NB + q], vn);
     }
-    zj[r] = zn;
-    if (pred) vj[r] = vn;
+    gst(zj + r, zn);
+    if (pred) gst(vj + r, vn);
     double zz = zn * zn, zv = zn * vn, vv = vn * vn;
     for (int o = 32; o >= 1; o >>= 1) {
       zz += __shfl_down(zz, o, 64);
@@ -387,10 +395,10 @@ __global__ __launch_bounds__(64) void k_diag_factor(const OiCell* __restrict__ c
     double al = 0.0;  // alpha_j = W_jj^T z_j starts the alpha = W^T z accumulation
     for (int q = 0; q < NB; ++q) {
       const double wv = Tt[r * 65 + q];
-      Wj[q * NB + r] = wv;  // W[q][r], row-major
+      gst(Wj + q * NB + r, wv);  // W[q][r], row-major
       al = fma(wv, Tt[NB * 65 + q], al);
     }
-    c.vec[c.T * NB + j * NB + r] = al;
+    gst(c.vec + c.T * NB + j * NB + r, al);
   }
 }
 
@@ -427,6 +435,37 @@ __device__ __forceinline__ void mfma16x16(d4& acc, const double* Am, int la, boo
   }
 }
 
+// broadcast lane l (0..15, a constant after unrolling) of every 16-lane row to
+// the whole row: DPP row_newbcast, a VALU move (no LDS round trip as __shfl)
+__device__ __forceinline__ int bcast16_i(int v, int l) {
+#define OI_RB(n) \
+  case n:        \
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + n, 0xF, 0xF, false);
+  switch (l) {
+    OI_RB(0) OI_RB(1) OI_RB(2) OI_RB(3) OI_RB(4) OI_RB(5) OI_RB(6) OI_RB(7)
+    OI_RB(8) OI_RB(9) OI_RB(10) OI_RB(11) OI_RB(12) OI_RB(13) OI_RB(14)
+    default: return __builtin_amdgcn_update_dpp(0, v, 0x15F, 0xF, 0xF, false);
+  }
+#undef OI_RB
+}
+__device__ __forceinline__ double bcast16(double v, int l) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = bcast16_i((int)(x & 0xffffffffLL), l);
+  const int hi = bcast16_i((int)(x >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+#ifndef OI_DIAG_RSQ
+#define OI_DIAG_RSQ 1
+#endif
+// stage timestamps for tools/diag_engine_probe (compiled in only there)
+#ifdef OI_DIAG_TIMING
+__device__ long long g_diag_stamps[16];
+#define DIAG_STAMP(k) \
+  do { if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_stamps[k] = clock64(); } while (0)
+#else
+#define DIAG_STAMP(k) do {} while (0)
+#endif
 __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__ cells,
                                                      const int32_t* __restrict__ list, int j) {
   // packed 16x16 blocks (row stride 17): Lb holds L_IK (I > K, 6 blocks), Ib the
@@ -439,32 +478,50 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
   double* Xs = lds16 + 16 * 272;      // 16 x 17
   const OiCell& c = cells[list[blockIdx.x]];
   if (j >= c.T || *c.status != OI_OK) return;
+  DIAG_STAMP(0);
   const int r = threadIdx.x, fr = r & 15, fk = r >> 4, blk = r >> 4;
   double* Y = tileL(c, j, j);
   double R[NB];
 #pragma unroll
-  for (int q = 0; q < NB; ++q) R[q] = Y[q * NB + r];  // row r of the column-major tile
-  bool ok = true;
+  for (int q = 0; q < NB; ++q) R[q] = gld(Y + q * NB + r);  // row r of the column-major tile
+  DIAG_STAMP(1);
+  // smallest pivot (minNum: a NaN pivot is passed over, as !(d <= 0) passes it);
+  // one v_min per column instead of a flag the compiler keeps 64 pivots for
+  double dmin = __builtin_inf();
   // ---------------- potrf by 16-column panels
+  // Entries above the diagonal are scratch until "clear the upper part" below:
+  // every lane scales and updates its whole row, so no lane-dependent selects
+  // guard the serial part (rows r < cc compute values nobody reads).
 #pragma unroll
   for (int J = 0; J < 4; ++J) {
     const int c0 = 16 * J;
 #pragma unroll
     for (int cc = c0; cc < c0 + 16; ++cc) {
       const double d = rdlane(R[cc], cc);
-      ok = ok && !(d <= 0.0);
+      dmin = fmin(dmin, d);
+#if OI_DIAG_RSQ
+      // 1/sqrt(d) by v_rsq_f64 + two Newton steps (<= 1 ulp); the column is
+      // scaled by it (as LAPACK dpotf2 scales by 1/ajj) and L_cc = d/sqrt(d):
+      // eight VALU ops per column where sqrt + an IEEE division take ~25
+      double il = __builtin_amdgcn_rsq(d);
+      il = fma(0.5 * il, fma(-d * il, il, 1.0), il);
+      il = fma(0.5 * il, fma(-d * il, il, 1.0), il);
+      const double l = d * il;
+      const double qd = R[cc] * il;
+#else
       const double l = sqrt(d);
-      const double lr = r > cc ? R[cc] / l : 0.0;
-      R[cc] = r > cc ? lr : (r == cc ? l : R[cc]);
+      const double qd = R[cc] / l;  // on every lane: no exec-mask branch
+#endif
+      R[cc] = r == cc ? l : qd;
 #pragma unroll
-      for (int s2 = cc + 1; s2 < c0 + 16; ++s2) R[s2] -= lr * rdlane(R[cc], s2);
+      for (int s2 = cc + 1; s2 < c0 + 16; ++s2) R[s2] -= qd * rdlane(R[cc], s2);
     }
     if (J == 3) break;
     // trailing update: A_IK -= P_I P_K^T for J < K <= I, P = rows of panel J
     double* P = lds16;              // 64 x 17
     double* U = lds16 + NB * 17;    // results: U[row * 49 + (s - c0 - 16)]
 #pragma unroll
-    for (int q = 0; q < 16; ++q) P[r * 17 + q] = r > c0 + q ? R[c0 + q] : (r == c0 + q ? R[c0 + q] : 0.0);
+    for (int q = 0; q < 16; ++q) P[r * 17 + q] = r >= c0 + q ? R[c0 + q] : 0.0;
     __syncthreads();
 #pragma unroll
     for (int I = J + 1; I < 4; ++I)
@@ -477,11 +534,14 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
       }
     __syncthreads();
 #pragma unroll
-    for (int s2 = c0 + 16; s2 < NB; ++s2)
-      if ((s2 >> 4) <= blk) R[s2] -= U[r * 49 + (s2 - c0 - 16)];
+    for (int s2 = c0 + 16; s2 < NB; ++s2) {  // selected, not branched (unwritten U entries are dropped)
+      const double u = U[r * 49 + (s2 - c0 - 16)];
+      R[s2] -= (s2 >> 4) <= blk ? u : 0.0;
+    }
     __syncthreads();  // P / U are rewritten by the next panel
   }
-  if (!ok) {
+  DIAG_STAMP(2);
+  if (dmin <= 0.0) {
     if (r == 0) {
       *c.status = OI_NOT_PD;
       if (g_debug)
@@ -490,13 +550,14 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     }
     return;
   }
-  double lg = 0.0;
+  double dg = 1.0;  // L_rr, picked out by selects: one log per lane, not one per q
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
-    if (q > r) R[q] = 0.0;                                   // clear the upper part
-    if (q == r) lg = (j * NB + r < c.n) ? log(R[q]) : 0.0;   // log L_rr
-    Y[q * NB + r] = R[q];                                    // L_jj, column-major
+    if (q > r) R[q] = 0.0;  // clear the upper part
+    dg = q == r ? R[q] : dg;
+    gst(Y + q * NB + r, R[q]);  // L_jj, column-major
   }
+  double lg = (j * NB + r < c.n) ? log(dg) : 0.0;  // log L_rr
   __syncthreads();  // lds16 held the potrf scratch
 #pragma unroll
   for (int K = 0; K < 4; ++K)  // L_IK blocks (I = blk > K), row-major for the MFMA A operand
@@ -510,21 +571,23 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
   }
   // ---------------- inverse: four diagonal 16x16 blocks at once (dtrti2 order)
+  DIAG_STAMP(3);
   double D[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q)  // D[q] = L[r][16 blk + q]
     D[q] = blk == 0 ? R[q] : blk == 1 ? R[16 + q] : blk == 2 ? R[32 + q] : R[48 + q];
 #pragma unroll
   for (int cc = 15; cc >= 0; --cc) {
-    const double ajj = 1.0 / __shfl(D[cc], cc, 16);
+    const double ajj = 1.0 / bcast16(D[cc], cc);
     double x = 0.0;
 #pragma unroll
-    for (int k = cc + 1; k < 16; ++k) x += D[k] * __shfl(D[cc], k, 16);
+    for (int k = cc + 1; k < 16; ++k) x += D[k] * bcast16(D[cc], k);
     D[cc] = fr > cc ? -ajj * x : (fr == cc ? ajj : D[cc]);
   }
 #pragma unroll
   for (int q = 0; q < 16; ++q) Ib[ib_index(blk, blk) * 272 + q * 17 + fr] = D[q];  // Inv_II (transposed)
   __syncthreads();
+  DIAG_STAMP(4);
   // ---------------- off-diagonal blocks by levels: Inv_IJ = -Inv_II X, X = sum_K L_IK Inv_KJ
 #pragma unroll
   for (int lev = 1; lev < 4; ++lev) {
@@ -554,7 +617,8 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
   }
   double* Dj = tileD(c, j);
 #pragma unroll
-  for (int q = 0; q < NB; ++q) Dj[q * NB + r] = R[q];  // column-major
+  for (int q = 0; q < NB; ++q) gst(Dj + q * NB + r, R[q]);  // column-major
+  DIAG_STAMP(5);
   // forward substitution, block j (see k_diag_factor)
   double zn = 0.0;
   {
@@ -570,8 +634,8 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
       zn = fma(R[q], Xs[q], zn);
       vn = fma(R[q], Xs[NB + q], vn);
     }
-    zj[r] = zn;
-    if (pred) vj[r] = vn;
+    gst(zj + r, zn);
+    if (pred) gst(vj + r, vn);
     double zz = zn * zn, zv = zn * vn, vv = vn * vn;
     for (int o = 32; o >= 1; o >>= 1) {
       zz += __shfl_down(zz, o, 64);
@@ -585,6 +649,7 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
       pp[2] = vv;
     }
   }
+  DIAG_STAMP(6);
   if (c.mode == OI_MODE_EVAL) {
     double* Wj = tileW(c, j, j);  // row-major W = L^-1: W[q][r] = Inv[q][r]
     __syncthreads();
@@ -595,11 +660,12 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
     double al = 0.0;  // alpha_j = W_jj^T z_j starts the alpha = W^T z accumulation
     for (int q = 0; q < NB; ++q) {
       const double wv = lds16[r * D16_LD + q];
-      Wj[q * NB + r] = wv;
+      gst(Wj + q * NB + r, wv);
       al = fma(wv, Xs[2 * NB + q], al);
     }
-    c.vec[c.T * NB + j * NB + r] = al;
+    gst(c.vec + c.T * NB + j * NB + r, al);
   }
+  DIAG_STAMP(7);
 }
 
 // ----------------------------------------------------------- k_scale(j)
@@ -625,8 +691,8 @@ __global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
 #pragma unroll
   for (int kk = 0; kk < NB / 4; ++kk) {
     const int q = kk * 4 + fk;
-    b0[kk] = D[q * NB + 32 * wc + fr];
-    b1[kk] = D[q * NB + 32 * wc + 16 + fr];
+    b0[kk] = gld(D + q * NB + 32 * wc + fr);
+    b1[kk] = gld(D + q * NB + 32 * wc + 16 + fr);
   }
   const int sm = t >> 2, sq = (t & 3) * 16;  // staging: column sm, rows sq..sq+15
   for (int k = k0; k < k0 + SCALE_KPW && k < j; ++k) {
@@ -634,9 +700,9 @@ __global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
     double v[16];
 #pragma unroll
     for (int u = 0; u < 16; u += 2) {
-      const double2 x = *(const double2*)(L + sm * NB + sq + u);
-      v[u] = x.x;
-      v[u + 1] = x.y;
+      const dv2 x = gload2(L + sm * NB + sq + u);
+      v[u] = x[0];
+      v[u + 1] = x[1];
     }
     __syncthreads();  // previous tile's reads of As are done
 #pragma unroll
@@ -658,7 +724,7 @@ __global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
       for (int nb = 0; nb < 2; ++nb)
         for (int r = 0; r < 4; ++r) {
           const int m = 32 * wr + 16 * mb + (lane >> 4) + 4 * r, n = 32 * wc + 16 * nb + (lane & 15);
-          P[m * NB + n] = -acc.c[mb][nb][r];  // D[m][n] = (Dinv L)[n][m] -> P[n][m]
+          gst(P + m * NB + n, -acc.c[mb][nb][r]);  // D[m][n] = (Dinv L)[n][m] -> P[n][m]
         }
   }
 }
@@ -724,7 +790,7 @@ __device__ __forceinline__ void fwd_update(const OiCell& c, const double* X, int
     const int h = t < 64 ? 0 : 1;
     double a = 0.0;
     for (int g = 0; g < G; ++g) a += red[(h * G + g) * NB + row];
-    c.vec[(h ? 3 * c.T * NB : 0) + i * NB + row] = pre - a;
+    gst(c.vec + (h ? 3 * c.T * NB : 0) + i * NB + row, pre - a);
   }
 }
 
@@ -760,7 +826,7 @@ __device__ __forceinline__ void alpha_update(const OiCell& c, const double* X, i
   if (t < 64) {
     double a = 0.0;
     for (int g = 0; g < G; ++g) a += red[g * NB + row];
-    c.vec[c.T * NB + jj * NB + row] = pre + a;
+    gst(c.vec + c.T * NB + jj * NB + row, pre + a);
   }
 }
 
@@ -806,7 +872,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
         for (int r = 0; r < 4; ++r) {
-          Y[acc1_row(mb, r) * NB + acc1_col(nb)] = acc.c[mb][nb][r];  // L_ij, column-major
+          gst(Y + acc1_row(mb, r) * NB + acc1_col(nb), acc.c[mb][nb][r]);  // L_ij, column-major
           lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // staged: X[col*XLD + row]
         }
     __syncthreads();
@@ -848,7 +914,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       for (int nb = 0; nb < 2; ++nb)
         for (int r = 0; r < 4; ++r) {
           const int m = acc1_row(mb, r), n = acc1_col(nb);
-          Yd[m * NB + n] = Yd[m * NB + n] - accd.c[mb][nb][r];
+          gst(Yd + m * NB + n, gld(Yd + m * NB + n) - accd.c[mb][nb][r]);
         }
     return;
   }
@@ -871,7 +937,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
       for (int r = 0; r < 4; ++r) {
-        Wt[acc1_row(mb, r) * NB + acc1_col(nb)] = acc.c[mb][nb][r];  // row-major
+        gst(Wt + acc1_row(mb, r) * NB + acc1_col(nb), acc.c[mb][nb][r]);  // row-major
         lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // X[row of W * XLD + col]
       }
   __syncthreads();
@@ -912,11 +978,11 @@ __device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, dou
   for (int e = threadIdx.x; e < OI_TILE; e += GEMM_THREADS) {
     const double v = X[(e >> 6) * XLD + (e & 63)];
     if (op == EMIT_STORE)
-      dst[e] = v;
+      gst(dst + e, v);
     else if (op == EMIT_SUB)
-      dst[e] = dst[e] - v;
+      gst(dst + e, gld(dst + e) - v);
     else
-      dst[e] = -v;
+      gst(dst + e, -v);
   }
 }
 
@@ -1235,6 +1301,8 @@ __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cel
   const OiCell& c = cells[list[blockIdx.x]];
   __shared__ double red[4 * 7];
   const int t = threadIdx.x, T = c.T, ntile = T * (T + 1) / 2;
+  // the round's status rides home in the result row (one D2H copy per round)
+  if (t == 0) c.out[OI_OUT_STATUS] = (double)*c.status;
   if (c.mode == OI_MODE_PREDICT) {
     // GPR:178-182 from the forward substitution run inside the factorisation:
     // z = L^-1 r, v = L^-1 k*: k*^T K^-1 r = v.z, k*^T K^-1 k* = v.v, r^T K^-1 r = z.z

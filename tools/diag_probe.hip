@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <cmath>
 #include <vector>
+#include <chrono>
+#include <algorithm>
 #define CHK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP error %s at %d\n",hipGetErrorString(e),__LINE__); exit(1);}}while(0)
 #define NB 64
 #define LD 65
@@ -171,6 +173,24 @@ int main() {
       printf("%-24s B=%5d  %8.2f us/launch\n", name, B, ms * 1e3 / reps);
     }
   };
+  // one launch at a time with the GPU idle in between (the single-cell engine's
+  // situation): per-launch events, host spin of GAP us between launches
+  auto gapped = [&](auto kern, const char* name, int gap_us) {
+    std::vector<float> v;
+    for (int k = 0; k < 60; ++k) {
+      CHK(hipEventRecord(e0));
+      hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, 0, A, L, D);
+      CHK(hipEventRecord(e1));
+      CHK(hipEventSynchronize(e1));
+      float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+      if (k >= 10) v.push_back(ms * 1e3f);
+      auto t0 = std::chrono::steady_clock::now();
+      while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() < gap_us) {}
+    }
+    std::sort(v.begin(), v.end());
+    printf("%-24s B=1 gap %4d us: p50 %8.2f us/launch (min %.2f)\n", name, gap_us, v[v.size() / 2], v[0]);
+  };
+  for (int g : {0, 50, 300, 2000}) gapped(kd<4>, "stage4 gapped", g);
   run(kd<0>, "stage0 load+store");
   run(kd<1>, "stage1 +potrf16");
   run(kd<2>, "stage2 +diag inverses");
