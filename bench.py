@@ -614,11 +614,11 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
 def main():
     args = parse()
     heartbeat()
-    # two resident-cell groups on two streams: one group's latency-bound launches
-    # (diagonal factors, scales) overlap the other's GEMMs and the host's round
-    # bookkeeping (+1 % on the day, profiles/r02/ab_*); per-cell results are
-    # unchanged (batch-independent arithmetic)
-    os.environ.setdefault('OI_GROUPS', '2')
+    # one resident-cell group (one stream): OI_GROUPS=2 overlaps one group's
+    # latency-bound launches with the other's GEMMs, +0.5 % on the day
+    # (profiles/r02/ab/), but the two streams' kernels then share the chip and
+    # the per-kernel HIP-event durations the roofline divides by stop being
+    # the kernel's own (frac 0.46 vs 0.61 on the same run)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
