@@ -577,6 +577,24 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
     fam_exec = sum(v['flops'] for k, v in kern.items() if fam_of.get(k) == fam) if fam else 0.0
     alg_dom = kd['flops'] * fam_alg[fam] / fam_exec if fam and fam_exec > 0 else kd['flops']
     achieved = alg_dom / (kd['total_ms'] / 1e3) / 1e12 if kd['total_ms'] > 0 else 0.0
+    # every GEMM kernel on the same footing (algorithmic and executed rates),
+    # and each family's executed / algorithmic flops (padding + O(T^2) products)
+    per_kernel = {}
+    for k, v in kern.items():
+        f = fam_of.get(k)
+        if not f or v['total_ms'] <= 0:
+            continue
+        fe = sum(x['flops'] for kk, x in kern.items() if fam_of.get(kk) == f)
+        alg = v['flops'] * fam_alg[f] / fe if fe > 0 else 0.0
+        per_kernel[k] = {"alg_tflops": round(alg / (v['total_ms'] / 1e3) / 1e12, 3),
+                         "frac": round(alg / (v['total_ms'] / 1e3) / 1e12 / PEAK_FP64_TFLOPS, 4),
+                         "exec_tflops": round(v['flops'] / (v['total_ms'] / 1e3) / 1e12, 3),
+                         "ms": round(v['total_ms'], 3)}
+    fam_ratio = {}
+    for f in ('factor', 'lauum'):
+        fe = sum(x['flops'] for kk, x in kern.items() if fam_of.get(kk) == f)
+        if fam_alg[f] > 0 and fe > 0:
+            fam_ratio[f] = round(fe / fam_alg[f], 4)
     traffic = None
     tfile = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tfile):
@@ -602,6 +620,8 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
             "executed_flops_per_launch": kd['flops'] / max(kd['launches'], 1),
             "executed_flop_model": "executed fp64 MFMA tile products, 2*64^3 each (padded 64x64 tiles)",
             "kernels_ms": {k: round(v['total_ms'], 3) for k, v in kern.items() if v['launches']},
+            "gemm_kernels": per_kernel,
+            "executed_over_algorithmic": fam_ratio,
             "useful_tflops_per_gpu": round(useful / dt / 1e12, 3),
             "useful_frac_per_gpu": round(useful / dt / 1e12 / PEAK_FP64_TFLOPS, 4),
             "useful_flop_model": "SURVEY §8d: E*(m^3+40m^2) + m^3/3 + 16m^2 per cell, m distinct sites",
