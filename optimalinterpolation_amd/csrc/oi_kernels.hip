@@ -455,6 +455,9 @@ __device__ __forceinline__ double bcast16(double v, int l) {
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
+#ifndef OI_LAUUM_EPI
+#define OI_LAUUM_EPI 1
+#endif
 #ifndef OI_DIAG_RSQ
 #define OI_DIAG_RSQ 1
 #endif
@@ -1143,6 +1146,10 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
         const int m = acc1_row(mb, r), nn = acc1_col(nb);
         const int a = i * NB + m, b = j * NB + nn;
         if (a >= n || b >= n || (i == j && m < nn)) continue;
+#if OI_LAUUM_EPI == 0  // timing experiments only (tools): no epilogue
+        s[3] += acc.c[mb][nb][r];
+        continue;
+#endif
         const double wgt = (a == b) ? 1.0 : 2.0;
         const double w0 = acc.c[mb][nb][r] - al[m] * al[64 + nn];  // (M^-1 - aa^T)_st
         const double w = (dl[m] * dl[64 + nn]) * w0;                // (D M^-1 D - uu^T)_st
@@ -1150,7 +1157,11 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
         const double d1 = uQ[1 * 128 + m] - uQ[1 * 128 + 64 + nn];
         const double d2 = uQ[2 * 128 + m] - uQ[2 * 128 + 64 + nn];
         const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+#if OI_LAUUM_EPI == 2  // timing experiments only (tools): no exp
+        const double e = 1.0 - Q;
+#else
         const double e = exp(-Q);
+#endif
         const double K = sf2 * ((1.0 + Q) * e);
         const double q0 = uq[0 * 128 + m] - uq[0 * 128 + 64 + nn];
         const double q1 = uq[1 * 128 + m] - uq[1 * 128 + 64 + nn];
