@@ -762,6 +762,13 @@ def main():
             "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
             "failed_cells": int(np.sum(status != 0)), "timed_s": round(dt, 3),
             "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float))}
+    rl = prof.get('rounds_log') or []
+    if rl:  # [n_eval, n_pred, maxT, sum T^3 of fitting cells, GPU ms] per round
+        tot = sum(r[4] for r in rl)
+        small = [r for r in rl if r[0] + r[1] < 256]
+        line["rounds"] = {"count": len(rl), "gpu_ms": round(tot, 1),
+                          "lt256_cells": len(small), "lt256_gpu_ms": round(sum(r[4] for r in small), 1),
+                          "note": "rounds with < 256 resident cells (the day's tail of slow-converging cells)"}
     dom = line["roofline"]["kernel"]
     pu, pt = prof_untimed.get(dom, {"launches": 0, "total_ms": 0.0}), prof["kernels"][dom]
     nall = pu["launches"] + pt["launches"]
