@@ -1525,10 +1525,8 @@ extern "C" int oi_launch_build(const OiCell* cells, const int32_t* list, int nce
 extern "C" int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j,
                                      void* stream) {
   if (ncell <= 0) return 0;
-  static const int variant = [] {
-    const char* e = getenv("OI_DIAG");
-    return e ? atoi(e) : 16;
-  }();
+  const char* ev = getenv("OI_DIAG");  // read per launch (tests switch it): ~0.1 us
+  const int variant = ev ? atoi(ev) : 16;
   if (variant == 32)  // the round-1 32-blocked kernel (A/B)
     hipLaunchKernelGGL(k_diag_factor, dim3(ncell), dim3(64), 0, S(stream), cells, list, j);
   else
@@ -1566,10 +1564,8 @@ extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, in
 extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                                     void* stream) {
   if (ncell <= 0 || maxT <= 0) return 0;
-  static const int variant = [] {
-    const char* e = getenv("OI_LAUUM");
-    return e ? atoi(e) : 1;
-  }();
+  const char* ev = getenv("OI_LAUUM");  // read per launch (tests switch it)
+  const int variant = ev ? atoi(ev) : 1;
   if (variant != 4) {  // one 64x64 tile per 256-thread workgroup (default: measured faster)
     const int gx = maxT * (maxT + 1) / 2;
     hipLaunchKernelGGL(k_lauum_grad1, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,

@@ -186,6 +186,16 @@ def test_panel_schemes_agree(scheme, monkeypatch):
         assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
 
 
+@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4')])
+def test_alternate_kernels_agree(knob, value, monkeypatch):
+    """The A/B alternates kept in the library -- round 1's 32-blocked diagonal
+    factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r) and the
+    128x128 K^-1 / gradient kernel (OI_LAUUM=4) -- meet the T1 tolerance on
+    tile-boundary sizes, fit and predict."""
+    monkeypatch.setenv(knob, value)
+    test_panel_schemes_agree('2', monkeypatch)
+
+
 def test_config5_size_n5000():
     """BASELINE config 5 allows n up to 5000 per cell (T = 79 tiles): SMLII and
     the predict block at that size, T1 tolerance, one cell each."""
