@@ -12,6 +12,7 @@
 // Measured on MI355X (tools/gemm_probe2.hip, v7): 63 TF/s with both operands
 // streamed from HBM vs 48.5 TF/s for a 256-thread 64x64 tile.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -67,12 +68,21 @@ struct StageRegs3 {
   dv2 a, b0, b1;
 };
 
+// Per-chunk masks (MASKED only): cmask(ch) returns more blocks to drop for
+// 16-deep chunk ch alone -- the structural zeros of a triangular operand
+// (Dinv_jj, W_jj,jj) in the pair that carries it, where whole chunks of k
+// meet only zeros for some of the wave's output blocks.  Evaluated once per
+// chunk and made wave-uniform (readfirstlane), like `skip`.
+struct NoChunkMask {
+  __device__ __forceinline__ unsigned operator()(int) const { return 0u; }
+};
+
 // MASKED: `skip` (wave-uniform, bit 2*mb + nb) drops this wave's 16x16
 // accumulator blocks that cover only padding rows / columns of a cell (their
 // exact result is 0, which the accumulator already holds).
-template <bool MASKED = false, class PairFn>
+template <bool MASKED = false, class PairFn, class CMask = NoChunkMask>
 __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs, PairFn pair,
-                                             unsigned skip = 0u) {
+                                             unsigned skip = 0u, CMask cmask = CMask()) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = (w >> 2) & 1, wc = w & 3;
   const int nch = npairs * (GNB / KC);  // even
@@ -96,9 +106,13 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
     *(dv2*)(Bs + sk * LDSB + sm) = q.b0;
     *(dv2*)(Bs + sk * LDSB + 64 + sm) = q.b1;
   };
-  auto compute = [&](int buf) __attribute__((always_inline)) {
+  auto compute = [&](int buf, int chunk) __attribute__((always_inline)) {
     const double* As = lds + buf * (STAGE_A + STAGE_B);
     const double* Bs = As + STAGE_A;
+    // a wave skips a chunk only when all four of its blocks are masked (one
+    // uniform branch per chunk; per-MFMA tests cost more than the partial
+    // blocks they save -- those compute exact zeros or unread entries)
+    if (MASKED && (skip | __builtin_amdgcn_readfirstlane(cmask(chunk))) == 0xFu) return;
 #pragma unroll
     for (int kk = 0; kk < KC / 4; ++kk) {
       const int k = kk * 4 + fk;
@@ -106,10 +120,10 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
       const double a1 = As[k * LDSA + 32 * wr + 16 + fr];
       const double b0 = Bs[k * LDSB + 32 * wc + fr];
       const double b1 = Bs[k * LDSB + 32 * wc + 16 + fr];
-      if (!MASKED || !(skip & 1u)) acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
-      if (!MASKED || !(skip & 2u)) acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
-      if (!MASKED || !(skip & 4u)) acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
-      if (!MASKED || !(skip & 8u)) acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+      acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+      acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+      acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+      acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
     }
   };
   load(0, r0);
@@ -121,11 +135,11 @@ __device__ __forceinline__ void gemm2_kmajor(Quad& acc, double* lds, int npairs,
   // paths and wait for the newest loads too, serialising the ring.
   for (int ch = 0; ch < nch; ch += 2) {
     load(min(ch + 2, nch - 1), r0);
-    compute(0);
+    compute(0, ch);
     store(1, r1);
     __syncthreads();
     load(min(ch + 3, nch - 1), r1);
-    compute(1);
+    compute(1, ch + 1);
     if (ch + 2 < nch) store(0, r0);
     __syncthreads();
   }
@@ -157,9 +171,9 @@ __device__ __forceinline__ int acc1_col(int nb) {
 // MASKED: `skip` (wave-uniform, bit 2*mb + nb) drops this wave's 16x16
 // accumulator blocks whose outputs are never used (the upper triangle of a
 // diagonal tile, padding rows / columns); their accumulators stay 0.
-template <bool MASKED = false, class PairFn>
+template <bool MASKED = false, class PairFn, class CMask = NoChunkMask>
 __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int nch, unsigned skip,
-                                             PairFn pair) {
+                                             PairFn pair, CMask cmask = CMask()) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = w >> 1, wc = w & 1;
   if (nch <= 0) return;
@@ -184,9 +198,15 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int nch, un
     *(dv2*)(Bs + sk * LDSA + sm) = q.b0;
     *(dv2*)(Bs + (sk + 8) * LDSA + sm) = q.b1;
   };
-  auto compute = [&](int buf) __attribute__((always_inline)) {
+  auto compute = [&](int buf, int chunk) __attribute__((always_inline)) {
     const double* As = lds + buf * 2 * STAGE_A;
     const double* Bs = As + STAGE_A;
+    // per-block tests (uniform branches): on this 256-thread core they cost
+    // less than the partial blocks they save (k_lauum_grad1 -2 %, k_chol_panel
+    // -10 %; the 512-thread gemm2 prefers whole-chunk skips)
+    unsigned sk = skip;
+    if (MASKED) sk |= __builtin_amdgcn_readfirstlane(cmask(chunk));
+    if (MASKED && sk == 0xFu) return;
 #pragma unroll
     for (int kk = 0; kk < KC / 4; ++kk) {
       const int k = kk * 4 + fk;
@@ -194,10 +214,10 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int nch, un
       const double a1 = As[k * LDSA + 32 * wr + 16 + fr];
       const double b0 = Bs[k * LDSA + 32 * wc + fr];
       const double b1 = Bs[k * LDSA + 32 * wc + 16 + fr];
-      if (!MASKED || !(skip & 1u)) acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
-      if (!MASKED || !(skip & 2u)) acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
-      if (!MASKED || !(skip & 4u)) acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
-      if (!MASKED || !(skip & 8u)) acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+      if (!MASKED || !(sk & 1u)) acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+      if (!MASKED || !(sk & 2u)) acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+      if (!MASKED || !(sk & 4u)) acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+      if (!MASKED || !(sk & 8u)) acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
     }
   };
   load(0, r0);
@@ -208,11 +228,11 @@ __device__ __forceinline__ void gemm1_kmajor(Quad& acc, double* lds, int nch, un
   // second half-step (the re-loaded duplicate is staged but never used)
   for (int ch = 0; ch < nch; ch += 2) {
     load(min(ch + 2, nch - 1), r0);
-    compute(0);
+    compute(0, ch);
     store(1, r1);
     __syncthreads();
     load(min(ch + 3, nch - 1), r1);
-    if (ch + 1 < nch) compute(1);
+    if (ch + 1 < nch) compute(1, ch + 1);
     if (ch + 2 < nch) store(0, r0);
     __syncthreads();
   }

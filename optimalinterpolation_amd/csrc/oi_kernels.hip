@@ -713,14 +713,20 @@ __global__ __launch_bounds__(256) void k_scale(const OiCell* __restrict__ cells,
     __syncthreads();
     Quad acc;
     quad_zero(acc);
+    // B(q, n) = Dinv[n][q] is 0 for q > n: k-steps past a block's last column are skipped
+    const int nlast = __builtin_amdgcn_readfirstlane(32 * wc) + 15;
 #pragma unroll
     for (int kk = 0; kk < NB / 4; ++kk) {
       const int q = kk * 4 + fk;
       const double a0 = As[q * LDSA + 32 * wr + fr], a1 = As[q * LDSA + 32 * wr + 16 + fr];
-      acc.c[0][0] = MFMA64(a0, b0[kk], acc.c[0][0]);
-      acc.c[0][1] = MFMA64(a0, b1[kk], acc.c[0][1]);
-      acc.c[1][0] = MFMA64(a1, b0[kk], acc.c[1][0]);
-      acc.c[1][1] = MFMA64(a1, b1[kk], acc.c[1][1]);
+      if (4 * kk <= nlast) {
+        acc.c[0][0] = MFMA64(a0, b0[kk], acc.c[0][0]);
+        acc.c[1][0] = MFMA64(a1, b0[kk], acc.c[1][0]);
+      }
+      if (4 * kk <= nlast + 16) {
+        acc.c[0][1] = MFMA64(a0, b1[kk], acc.c[0][1]);
+        acc.c[1][1] = MFMA64(a1, b1[kk], acc.c[1][1]);
+      }
     }
     double* P = c.P + (size_t)k * OI_TILE;
     for (int mb = 0; mb < 2; ++mb)
@@ -740,6 +746,55 @@ __device__ __forceinline__ unsigned pad_skip(int m0, int n0, int mlim, int nlim)
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
       if (m0 + 16 * mb >= mlim || n0 + 16 * nb >= nlim) s |= 1u << (2 * mb + nb);
+  return s;
+}
+
+// Structural zeros of triangular operands, per 16-deep k-chunk c, for a
+// wave's 2 x 2 blocks (bit 2*mb + nb) at output rows r0 + 16 mb and columns
+// c0 + 16 nb (gemm cores: acc(m, n) += A(m, k) B(k, n)):
+//   A(m, k) = 0 for k < m (W_jj,jj as the A operand): rows_below
+//   A(m, k) = 0 for k > m (Dinv_jj, column-major, as A):  rows_above
+//   B(k, n) = 0 for k < n (W_jj,jj as B):                  cols_below
+//   B(k, n) = 0 for k > n (Dinv_jj^T as B):                cols_above
+// The skipped products are exact zeros, so results do not change.
+__device__ __forceinline__ unsigned rows_below(int c, int r0) {
+  unsigned s = 0;
+  for (int mb = 0; mb < 2; ++mb)
+    if (16 * c + 15 < r0 + 16 * mb) s |= 3u << (2 * mb);
+  return s;
+}
+__device__ __forceinline__ unsigned rows_above(int c, int r0) {
+  unsigned s = 0;
+  for (int mb = 0; mb < 2; ++mb)
+    if (16 * c > r0 + 16 * mb + 15) s |= 3u << (2 * mb);
+  return s;
+}
+__device__ __forceinline__ unsigned cols_below(int c, int c0) {
+  unsigned s = 0;
+  for (int nb = 0; nb < 2; ++nb)
+    if (16 * c + 15 < c0 + 16 * nb) s |= 5u << nb;
+  return s;
+}
+__device__ __forceinline__ unsigned cols_above(int c, int c0) {
+  unsigned s = 0;
+  for (int nb = 0; nb < 2; ++nb)
+    if (16 * c > c0 + 16 * nb + 15) s |= 5u << nb;
+  return s;
+}
+// accumulator blocks strictly above (m < n) / below (m > n) the diagonal of a
+// symmetric (syrk) output tile
+__device__ __forceinline__ unsigned upper_blocks(int r0, int c0) {
+  unsigned s = 0;
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb)
+      if (r0 + 16 * mb + 15 < c0 + 16 * nb) s |= 1u << (2 * mb + nb);
+  return s;
+}
+__device__ __forceinline__ unsigned lower_blocks(int r0, int c0) {
+  unsigned s = 0;
+  for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < 2; ++nb)
+      if (r0 + 16 * mb > c0 + 16 * nb + 15) s |= 1u << (2 * mb + nb);
   return s;
 }
 
@@ -867,10 +922,11 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       b = tileL(c, i, k);  // k == j: A_ij, already holding A_ij - sum_{k<kbeg} L_ik L_jk^T
     };
     const double pre = fwd_preload(c, i, j);
-    if (i == T - 1 && rT < NB)  // n = row of block row i
-      gemm1_kmajor<true>(acc, lds, 4 * (j + 1 - kbeg), pad_skip(32 * wr, 32 * wc, NB, rT), fpair);
-    else
-      gemm1_kmajor<false>(acc, lds, 4 * (j + 1 - kbeg), 0u, fpair);
+    const int chD = 4 * (j - kbeg);  // first chunk of the Dinv_jj pair (A(m, k) = 0 for k > m)
+    auto cm = [=](int ch) { return ch >= chD ? rows_above(ch - chD, 32 * wr) : 0u; };
+    // n = row of block row i: padding rows of the last block are skipped
+    gemm1_kmajor<true>(acc, lds, 4 * (j + 1 - kbeg), i == T - 1 ? pad_skip(32 * wr, 32 * wc, NB, rT) : 0u,
+                       fpair, cm);
     double* Y = tileL(c, i, j);
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
@@ -908,7 +964,10 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       }
     }
     __syncthreads();
-    GEMM1(accd, lds, j, [=, &c](int p, const double*& a, const double*& b) {
+    // symmetric, and only its lower triangle is read (k_diag_factor): accd(m, n)
+    // lands at row n, column m of the column-major tile, so the accumulator
+    // blocks with m > n -- the tile's upper triangle -- are skipped
+    gemm1_kmajor<true>(accd, lds, 4 * j, lower_blocks(32 * wr, 32 * wc), [=, &c](int p, const double*& a, const double*& b) {
       a = tileL(c, i, p);
       b = a;
     });
@@ -932,10 +991,14 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
     b = tileW(c, k, jj);  // k == j: Vneg
   };
   const double apre = alpha_preload(c, jj, j);
-  if (j == T - 1 && rT < NB)  // m = row of W block row j
-    gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst + extra), pad_skip(32 * wr, 32 * wc, rT, NB), wpair);
-  else
-    gemm1_kmajor<false>(acc, lds, 4 * (j - kfirst + extra), 0u, wpair);
+  // pair k = jj: B = W_jj,jj (B(k, n) = 0 for k < n); pair k = j: A = Dinv_jj
+  const int chD = extra ? 4 * (j - kfirst) : 1 << 30;
+  auto cm = [=](int ch) {
+    return (!extra && ch < 4 ? cols_below(ch, 32 * wc) : 0u) | (ch >= chD ? rows_above(ch - chD, 32 * wr) : 0u);
+  };
+  // m = row of W block row j: padding rows of the last block are skipped
+  gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst + extra), j == T - 1 ? pad_skip(32 * wr, 32 * wc, rT, NB) : 0u,
+                     wpair, cm);
   double* Wt = tileW(c, j, jj);
   for (int mb = 0; mb < 2; ++mb)
     for (int nb = 0; nb < 2; ++nb)
@@ -1025,10 +1088,14 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
     // m = row of block row i; half 1's n = column of block column j+1
     const int mlim = i == T - 1 ? rT : NB, nlim = (wc >= 2 && j + 1 == T - 1) ? rT : NB;
     const double pre = fwd_preload(c, i, j);
-    if (mlim < NB || nlim < NB)
-      gemm2_kmajor<true>(acc, lds, j + 1, fpair, pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim));
-    else
-      gemm2_kmajor<false>(acc, lds, j + 1, fpair);
+    // last pair: half 0 multiplies by Dinv_jj^T (B(k, n) = 0 for k > n), half 1 by
+    // the zero tile; the first row's half 1 (x = 0) is the diagonal tile j+1,
+    // symmetric: its blocks above the diagonal are never read
+    const int chD = 4 * j;
+    const unsigned sk = pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim) |
+                        (x == 0 && wc >= 2 ? upper_blocks(32 * wr, 32 * (wc - 2)) : 0u);
+    auto cm = [=](int ch) { return ch < chD ? 0u : wc >= 2 ? 0xFu : cols_above(ch - chD, 32 * wc); };
+    gemm2_kmajor<true>(acc, lds, j + 1, fpair, sk, cm);
     emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij (staged in lds as X[col*XLD+row])
     fwd_update<GEMM_THREADS>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) {
@@ -1069,10 +1136,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   // n = row of W block row j (half 0) or j+1 (half 1)
   const int nlim = ((wc < 2 && j == T - 1) || (wc >= 2 && j + 1 == T - 1)) ? rT : NB;
   const double apre = alpha_preload(c, jj, j);
-  if (nlim < NB)
-    gemm2_kmajor<true>(acc, lds, j - jj, wpair, pad_skip(0, 32 * (wc & 1), NB, nlim));
-  else
-    gemm2_kmajor<false>(acc, lds, j - jj, wpair);
+  // pair k = jj: A = W_jj,jj^T (A(m, k) = 0 for k < m); no row j+1: half 1 idle
+  const unsigned sk = pad_skip(0, 32 * (wc & 1), NB, nlim) | (!has_next && wc >= 2 ? 0xFu : 0u);
+  auto cm = [=](int ch) { return ch < 4 ? rows_below(ch, 32 * wr) : 0u; };
+  gemm2_kmajor<true>(acc, lds, j - jj, wpair, sk, cm);
   emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);           // W_j,jj (row-major), staged X[n*XLD+m]
   alpha_update<GEMM_THREADS>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
   if (has_next) emit_half(acc, 1, lds, tileW(c, j + 1, jj), EMIT_NEG);  // Vneg
@@ -1116,10 +1183,9 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
     a = tileW(c, i + p, i);
     b = tileW(c, i + p, j);
   };
-  if (i == j || i == T - 1)
-    gemm1_kmajor<true>(acc, lds, nch, skip, wpair);
-  else
-    gemm1_kmajor<false>(acc, lds, nch, 0u, wpair);
+  // pair k = i: A = W_ii^T (A(m, k) = 0 for k < m), and B = W_ii too on the diagonal
+  auto cm = [=](int ch) { return ch < 4 ? rows_below(ch, 32 * wr) | (i == j ? cols_below(ch, 32 * wc) : 0u) : 0u; };
+  gemm1_kmajor<true>(acc, lds, nch, skip, wpair, cm);
   double* uQ = lds;            // [3][128]: rows 0..63, columns 64..127
   double* uq = lds + 3 * 128;  // [3][128]
   double* al = lds + 6 * 128;  // [128]
