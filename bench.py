@@ -775,6 +775,7 @@ def main():
     if rl:  # [n_eval, n_pred, maxT, sum T^3 of fitting cells, GPU ms] per round
         tot = sum(r[4] for r in rl)
         small = [r for r in rl if r[0] + r[1] < 256]
+        line["host"] = {k: round(prof.get(k, 0.0), 3) for k in ('wall_s', 'sync_s', 'consume_s', 'prep_s', 'launch_s')}
         line["rounds"] = {"count": len(rl), "gpu_ms": round(tot, 1),
                           "lt256_cells": len(small), "lt256_gpu_ms": round(sum(r[4] for r in small), 1),
                           "note": "rounds with < 256 resident cells (the day's tail of slow-converging cells)"}

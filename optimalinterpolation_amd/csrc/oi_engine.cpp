@@ -144,6 +144,9 @@ struct RunStat {
   double wall_s = 0.0;
   double setup_s = 0.0;  // run() entry -> first round (uploads, residuals)
   double sync_s = 0.0;   // host blocked on round completion
+  double consume_s = 0.0;  // consume(): sync + results + coroutine steps
+  double prep_s = 0.0;     // launch_round() before its first kernel (lists, sort, copy)
+  double launch_s = 0.0;   // launch_round() in total (incl. every launch call)
 } g_run;
 struct LaunchRec {
   int kind, j, cells;
@@ -617,6 +620,7 @@ class Engine {
   }
 
   void launch_round(Group& gr) {
+    const auto tl0 = std::chrono::steady_clock::now();
     hipStream_t gst = gr.st;
     auto hc = [&](int s) -> OiCell& { return gr.hc[s - gr.s0]; };
     gr.ev_slots.clear();
@@ -680,6 +684,7 @@ class Engine {
     const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
     int rc = 0;
     cur_cells = na;
+    prep_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
     mark(K_BUILD, false);
     rc |= oi_launch_build(dc, dl_all, na, maxT, gst);
     mark(K_BUILD, true);
@@ -747,6 +752,7 @@ class Engine {
       }
     }
     gr.inflight = true;
+    launch_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
   }
 
   void consume(Group& gr) {
@@ -829,6 +835,7 @@ class Engine {
       }
     }
     gr.active.swap(still);
+    consume_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts0).count();
   }
 
   void flush_stats() {
@@ -847,8 +854,11 @@ class Engine {
     g_run.predicts += predicts_;
     g_run.sync_s += sync_s_;
     g_run.wall_s += wall_s_;
+    g_run.consume_s += consume_s_;
+    g_run.prep_s += prep_s_;
+    g_run.launch_s += launch_s_;
     rounds_ = evals_ = predicts_ = 0;
-    sync_s_ = wall_s_ = 0.0;
+    sync_s_ = wall_s_ = consume_s_ = prep_s_ = launch_s_ = 0.0;
   }
 
   Context& ctx_;
@@ -870,6 +880,7 @@ class Engine {
   int64_t kln_[K_COUNT] = {0};
   int64_t rounds_ = 0, evals_ = 0, predicts_ = 0;
   double sync_s_ = 0.0, wall_s_ = 0.0;
+  double consume_s_ = 0.0, prep_s_ = 0.0, launch_s_ = 0.0;  // host time per phase
   std::chrono::steady_clock::time_point t_start_;
 };
 
@@ -1113,12 +1124,12 @@ int64_t oi_profile_json(char* buf, int64_t len) {
                   e.second.bytes);
     s += tmp;
   }
-  char tmp[256];
+  char tmp[512];
   std::snprintf(tmp, sizeof(tmp),
                 "},\"rounds\":%lld,\"evals\":%lld,\"predicts\":%lld,\"wall_s\":%.6f,\"sync_s\":%.6f,"
-                "\"setup_s\":%.6f",
+                "\"setup_s\":%.6f,\"consume_s\":%.6f,\"prep_s\":%.6f,\"launch_s\":%.6f",
                 (long long)g_run.rounds, (long long)g_run.evals, (long long)g_run.predicts,
-                g_run.wall_s, g_run.sync_s, g_run.setup_s);
+                g_run.wall_s, g_run.sync_s, g_run.setup_s, g_run.consume_s, g_run.prep_s, g_run.launch_s);
   s += tmp;
   s += ",\"last_round\":[";
   for (size_t q = 0; q < g_last_round.size(); ++q) {
