@@ -698,10 +698,16 @@ class Engine {
       mark(K_CHOL, true);
       const bool even = !legacy_ && (j % 2 == 0);
       const int kbeg = (legacy_ || even) ? 0 : j - 1;
-      mark(K_SCALE, false);
-      rc |= oi_launch_scale(dc, dl_all, cnt, j, kbeg, gst);
-      mark(K_SCALE, true);
-      if (even) {
+      if (j > kbeg) {  // P_jk for kbeg <= k < j: nothing to scale at j = 0
+        mark(K_SCALE, false);
+        rc |= oi_launch_scale(dc, dl_all, cnt, j, kbeg, gst);
+        mark(K_SCALE, true);
+      }
+      // the last column of a round with no fitting cell has neither factor
+      // tiles below the diagonal nor a W row: its panel launch would be empty
+      const bool empty_panel = j == maxT - 1 && ne == 0;
+      if (empty_panel) {
+      } else if (even) {
         mark(K_EVEN, false);
         rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
         mark(K_EVEN, true);
