@@ -618,7 +618,9 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
             "achieved_executed": round(achieved_exec, 3),
             "frac_executed": round(achieved_exec / PEAK_FP64_TFLOPS, 4),
             "executed_flops_per_launch": kd['flops'] / max(kd['launches'], 1),
-            "executed_flop_model": "executed fp64 MFMA tile products, 2*64^3 each (padded 64x64 tiles)",
+            "executed_flop_model": ("executed fp64 MFMA flops: the 16x16 blocks x 16-deep chunks the kernels issue "
+                                    "(padding, triangular-operand and zero chunks they skip are not counted; the "
+                                    "engine mirrors the kernels' masks, oi_masks.h)"),
             "kernels_ms": {k: round(v['total_ms'], 3) for k, v in kern.items() if v['launches']},
             "gemm_kernels": per_kernel,
             "executed_over_algorithmic": fam_ratio,

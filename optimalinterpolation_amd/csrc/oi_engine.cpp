@@ -28,6 +28,7 @@
 #include "../../include/oi.h"
 #include "cg.hpp"
 #include "oi_device.h"
+#include "oi_masks.h"
 
 namespace {
 
@@ -132,6 +133,130 @@ bool legacy_panels() {
   const char* e = getenv("OI_PANEL");
   return e && atoi(e) == 1;
 }
+// Executed MFMA flops per cell and launch (profile mode), mirroring the
+// kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
+// 16-deep k-chunk is 8192 flops.  gemm2 (k_panel_even: 8 waves, wr 0..1,
+// wc 0..3) skips whole chunks only; gemm1 (k_chol_panel, k_lauum_grad1: 4
+// waves) skips per block.  Every count is closed-form in the cell's tile
+// geometry (O(T) per round at most).
+namespace acct {
+constexpr double BLK = 2.0 * 16 * 16 * 16;
+inline int live(unsigned m) { return __builtin_popcount(~m & 0xFu); }
+
+double panel_even(int T, int n, int j, bool eval) {
+  const int rT = n - OI_NB * (T - 1), nf = T - 1 - j;
+  auto factor_wg = [&](int x) {
+    const int i = j + 1 + x, mlim = i == T - 1 ? rT : OI_NB;
+    double b = 0;
+    for (int w = 0; w < 8; ++w) {
+      const int wr = (w >> 2) & 1, wc = w & 3;
+      const int nlim = (wc >= 2 && j + 1 == T - 1) ? rT : OI_NB;
+      const unsigned s = pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim) |
+                         (x == 0 && wc >= 2 ? upper_blocks(32 * wr, 32 * (wc - 2)) : 0u);
+      if (s == 0xFu) continue;
+      b += 16.0 * j;  // pairs p < j: 4 chunks x 4 blocks each
+      for (int c = 0; c < 4; ++c)
+        if ((s | (wc >= 2 ? 0xFu : cols_above(c, 32 * wc))) != 0xFu) b += 4;
+    }
+    if (x == 0) b += 64;  // the fresh L_j+1,j L_j+1,j^T product of the look-ahead
+    return b;
+  };
+  double blocks = 0;
+  if (nf > 0) blocks += factor_wg(0);
+  if (nf > 1) blocks += factor_wg(nf - 1);
+  if (nf > 2) blocks += (nf - 2) * factor_wg(1);
+  if (eval && j > 0) {
+    const bool has_next = j + 1 < T;
+    for (int w = 0; w < 8; ++w) {
+      const int wr = (w >> 2) & 1, wc = w & 3;
+      const int nlim = ((wc < 2 && j == T - 1) || (wc >= 2 && j + 1 == T - 1)) ? rT : OI_NB;
+      const unsigned s = pad_skip(0, 32 * (wc & 1), OI_NB, nlim) | (!has_next && wc >= 2 ? 0xFu : 0u);
+      if (s == 0xFu) continue;
+      double first = 0;  // the pair k = jj (W_jj,jj): its 4 chunks
+      for (int c = 0; c < 4; ++c)
+        if ((s | rows_below(c, 32 * wr)) != 0xFu) first += 4;
+      blocks += 16.0 * (j * (j - 1) / 2.0) + j * first;
+    }
+  }
+  return blocks * BLK;
+}
+
+double chol_panel(int T, int n, int j, int kbeg, bool eval) {
+  const int rT = n - OI_NB * (T - 1), nf = T - 1 - j;
+  auto factor_wg = [&](int x) {
+    const int i = j + 1 + x;
+    double b = 0;
+    for (int w = 0; w < 4; ++w) {
+      const int wr = w >> 1, wc = w & 1;
+      const unsigned s = i == T - 1 ? pad_skip(32 * wr, 32 * wc, OI_NB, rT) : 0u;
+      b += 4.0 * (j - kbeg) * live(s);
+      for (int c = 0; c < 4; ++c) b += live(s | rows_above(c, 32 * wr));  // the Dinv_jj pair
+      if (x == 0) b += 4.0 * j * live(lower_blocks(32 * wr, 32 * wc));  // look-ahead syrk
+    }
+    if (x == 0) b += 64;  // its fresh L_ij L_ij^T product
+    return b;
+  };
+  double blocks = 0;
+  if (nf > 0) blocks += factor_wg(0);
+  if (nf > 1) blocks += factor_wg(nf - 1);
+  if (nf > 2) blocks += (nf - 2) * factor_wg(1);
+  if (eval && j > 0) {
+    for (int w = 0; w < 4; ++w) {
+      const int wr = w >> 1, wc = w & 1;
+      const unsigned s = j == T - 1 ? pad_skip(32 * wr, 32 * wc, rT, OI_NB) : 0u;
+      // pair k = jj (B = W_jj,jj) when the tile starts there, pair k = j (A = Dinv_jj)
+      double tri_first = 0, dinv_last = 0;
+      for (int c = 0; c < 4; ++c) {
+        tri_first += live(s | cols_below(c, 32 * wc));
+        dinv_last += live(s | rows_above(c, 32 * wr));
+      }
+      for (int jj = 0; jj < j && jj < kbeg; ++jj)  // extra pair: k = kbeg .. j
+        blocks += 4.0 * (j - kbeg) * live(s) + dinv_last;
+      // kfirst = jj (jj >= kbeg): pairs k = jj .. j-1, the first against W_jj,jj
+      const int lo = kbeg < j ? kbeg : j;
+      for (int jj = lo; jj < j; ++jj) blocks += 4.0 * (j - jj - 1) * live(s) + tri_first;
+    }
+  }
+  return blocks * BLK;
+}
+
+// k_scale: per tile, B(q, n) = Dinv[n][q] is zero past the block's last column
+double scale_tile() {
+  double mfma = 0;
+  for (int wc = 0; wc < 2; ++wc)
+    for (int nb = 0; nb < 2; ++nb) mfma += 2 * 2 * std::min(16, (32 * wc + 16 * nb + 15) / 4 + 1);
+  return mfma * 2.0 * 16 * 16 * 4;
+}
+
+double lauum(int T, int n) {
+  const int rT = n - OI_NB * (T - 1);
+  double blocks = 0;
+  for (int i = 0; i < T; ++i) {
+    const int nch = 4 * (T - i - 1) + (rT + 15) / 16;
+    for (int diag = 0; diag < 2; ++diag) {  // tile (i, i), then one of the i tiles (i, j < i)
+      if (!diag && i == 0) continue;
+      const int jt = diag ? i : 0;
+      double b = 0;
+      for (int w = 0; w < 4; ++w) {
+        const int wr = w >> 1, wc = w & 1;
+        unsigned s = 0;
+        for (int mb = 0; mb < 2; ++mb)
+          for (int nb = 0; nb < 2; ++nb) {
+            const int m0 = 32 * wr + 16 * mb, n0 = 32 * wc + 16 * nb;
+            if ((diag && m0 + 15 < n0) || (i == T - 1 && m0 >= rT) || (jt == T - 1 && n0 >= rT))
+              s |= 1u << (2 * mb + nb);
+          }
+        for (int c = 0; c < nch && c < 4; ++c)
+          b += live(s | rows_below(c, 32 * wr) | (diag ? cols_below(c, 32 * wc) : 0u));
+        if (nch > 4) b += (nch - 4.0) * live(s);
+      }
+      blocks += diag ? b : i * b;
+    }
+  }
+  return blocks * BLK;
+}
+}  // namespace acct
+
 struct KStat {
   int64_t launches = 0;
   double ms = 0.0;
@@ -681,7 +806,7 @@ class Engine {
       const size_t idx = 2 * (gr.ev_kind.size() - 1) + (end ? 1 : 0);
       if (idx < gr.ev.size()) HIPC(hipEventRecord(gr.ev[idx], gst));
     };
-    const double tf = 2.0 * OI_NB * OI_NB * OI_NB;
+    static const double scale_fl = acct::scale_tile();
     int rc = 0;
     cur_cells = na;
     prep_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
@@ -716,23 +841,17 @@ class Engine {
         rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, gst);
         mark(K_TRSM, true);
       }
-      if (o_.profile) {  // executed MFMA flops: 2*64^3 per 64x64 tile product
+      if (o_.profile) {  // executed MFMA flops, mirroring the kernels' masks (acct::)
         for (int k = 0; k < cnt; ++k) {
           const OiCell& cd = hc(all_slots[k]);
           const bool ev = cd.mode == OI_MODE_EVAL;
-          kfl_[K_SCALE] += tf * (double)(j - kbeg);
-          if (even) {  // 64x128 blocks: two products per streamed pair
-            kfl_[K_EVEN] += tf * 2.0 * (double)(cd.T - 1 - j) * (j + 1);
-            if (cd.T - 1 - j > 0) kfl_[K_EVEN] += tf;  // fresh look-ahead product
-            if (ev)
-              for (int jj = 0; jj < j; ++jj) kfl_[K_EVEN] += tf * 2.0 * (double)(j - jj);
-          } else {
-            kfl_[K_TRSM] += tf * (double)(cd.T - 1 - j) * (j + 1 - kbeg);
-            if (cd.T - 1 - j > 0) kfl_[K_TRSM] += tf * (double)(j + 1);  // look-ahead diagonal
-            if (ev)
-              for (int jj = 0; jj < j; ++jj)
-                kfl_[K_TRSM] += tf * (double)(j - std::max(jj, kbeg) + (kbeg > jj ? 1 : 0));
-          }
+          if (j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
+          if (empty_panel)
+            continue;
+          else if (even)
+            kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev);
+          else
+            kfl_[K_TRSM] += acct::chol_panel(cd.T, cd.n, j, kbeg, ev);
         }
       }
     }
@@ -754,7 +873,7 @@ class Engine {
     if (o_.profile) {
       for (int k = 0; k < ne; ++k) {
         const OiCell& cd = hc(gr.ev_slots[k]);
-        for (int i = 0; i < cd.T; ++i) kfl_[K_LAUUM] += tf * (double)(cd.T - i) * (i + 1);
+        kfl_[K_LAUUM] += acct::lauum(cd.T, cd.n);
       }
     }
     gr.inflight = true;

@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(256) k_nys_grad_mfma(const double* __restrict_
   const int j = tile - i * (i + 1) / 2;
   Quad acc;
   quad_zero(acc);
-  gemm1_kmajor(acc, lds, Tk, [=](int p, const double*& a, const double*& b) {
+  gemm1_kmajor<false>(acc, lds, 4 * Tk, 0u, [=](int p, const double*& a, const double*& b) {
     a = Wp + ((size_t)p * Tn + i) * 4096;
     b = Wp + ((size_t)p * Tn + j) * 4096;
   });
