@@ -75,6 +75,9 @@ def parse():
                    help='skip the untimed priming call (profiler runs: every dispatch is then a timed one)')
     p.add_argument('--cpu-cores', type=int, default=0,
                    help='CPU baseline worker processes; 0: the host cores this process may use')
+    p.add_argument('--timed-profile', default='auto', choices=['auto', 'on', 'off'],
+                   help='per-launch HIP events inside the timed region (auto: on for day/days; off for '
+                        'single/predict, whose roofline then comes from a second, profiled pass)')
     p.add_argument('--out', default='')
     return p.parse_args()
 
@@ -685,7 +688,8 @@ def main():
         _lib.gpr_batch(prime.xyt, prime.z, prime.offs, prime.xs, prime.mean, x0=X0, opt=True, device=gpu,
                        profile=True)
     single = args.workload == 'single'
-    sess = None if single else _lib.Session(device=gpu, device_inputs=True, profile=True, max_pool=args.max_pool)
+    tprof = (args.workload in ('day', 'days')) if args.timed_profile == 'auto' else args.timed_profile == 'on'
+    sess = None if single else _lib.Session(device=gpu, device_inputs=True, profile=tprof, max_pool=args.max_pool)
     if single:  # config 1: blocking one-shot calls (per-cell latency)
         for item in dev_warm:
             cells, xyt, z, h = item
@@ -755,6 +759,13 @@ def main():
             cells, xyt, z, h = dev_slices[k]
             _lib.gpr_batch_device(xyt, z, cells.offs, cells.xs, cells.mean, x0=X0, opt=True, device=gpu,
                                   profile=True)
+    elif not tprof:  # the same slices again through a profiled session, untimed
+        _lib.profile_reset()
+        psess = _lib.Session(device=gpu, device_inputs=True, profile=True, max_pool=args.max_pool)
+        for k in range(done_k):
+            submit(psess, dev_slices[k])
+        psess.wait(-1)
+        psess.close()
     prof = _lib.profile_json()
     info = np.concatenate([outs[k][2] for k in range(done_k)])
     status = np.concatenate([outs[k][1] for k in range(done_k)])
@@ -770,7 +781,7 @@ def main():
             "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
             "failed_cells": int(np.sum(status != 0)), "timed_s": round(dt, 3),
             "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float))}
-    if single:
+    if not tprof:
         line["roofline"]["timing_note"] = ("per-launch HIP-event times from a second, profiled pass over the "
                                            "same cells; the timed pass runs without per-launch events")
     rl = prof.get('rounds_log') or []

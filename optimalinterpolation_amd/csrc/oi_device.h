@@ -82,10 +82,12 @@ int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int max
 int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
 int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j, int kbeg,
                     void* stream);
+// pform = 1: the P-form panels (P_jk = -Dinv_jj L_jk from k_scale streamed in
+// the GEMM loop); 0 (default): post-form, Dinv_jj applied to the finished sum
 int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                         int kbeg, int with_trtri, void* stream);
+                         int kbeg, int with_trtri, int pform, void* stream);
 int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                         int with_trtri, void* stream);
+                         int with_trtri, int pform, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                          void* stream);
 int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, void* stream);

@@ -133,6 +133,15 @@ bool legacy_panels() {
   const char* e = getenv("OI_PANEL");
   return e && atoi(e) == 1;
 }
+// Panel form, read per call from OI_PFORM:
+//   0 (default): post-form -- the panels stream L_jk and apply Dinv_jj once to
+//                the finished sum (post_left / post_right): no k_scale launch;
+//   1          : P-form -- k_scale writes P_jk = -Dinv_jj L_jk, streamed by the
+//                panels with A_ij Dinv_jj^T as the GEMM loop's last pair.
+bool pform_panels() {
+  const char* e = getenv("OI_PFORM");
+  return e && atoi(e) == 1;
+}
 // Executed MFMA flops per cell and launch (profile mode), mirroring the
 // kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
 // 16-deep k-chunk is 8192 flops.  gemm2 (k_panel_even: 8 waves, wr 0..1,
@@ -143,7 +152,12 @@ namespace acct {
 constexpr double BLK = 2.0 * 16 * 16 * 16;
 inline int live(unsigned m) { return __builtin_popcount(~m & 0xFu); }
 
-double panel_even(int T, int n, int j, bool eval) {
+// post_right / post_left (post-form): the triangular product S Dinv^T /
+// Dinv S of one tile, 160 MFMAs of 16x16x4 over the workgroup's waves (no
+// masks), in BLK units
+constexpr double POST_BLOCKS = 160.0 / 4.0;
+
+double panel_even(int T, int n, int j, bool eval, bool post) {
   const int rT = n - OI_NB * (T - 1), nf = T - 1 - j;
   auto factor_wg = [&](int x) {
     const int i = j + 1 + x, mlim = i == T - 1 ? rT : OI_NB;
@@ -155,10 +169,12 @@ double panel_even(int T, int n, int j, bool eval) {
                          (x == 0 && wc >= 2 ? upper_blocks(32 * wr, 32 * (wc - 2)) : 0u);
       if (s == 0xFu) continue;
       b += 16.0 * j;  // pairs p < j: 4 chunks x 4 blocks each
-      for (int c = 0; c < 4; ++c)
-        if ((s | (wc >= 2 ? 0xFu : cols_above(c, 32 * wc))) != 0xFu) b += 4;
+      if (!post)
+        for (int c = 0; c < 4; ++c)
+          if ((s | (wc >= 2 ? 0xFu : cols_above(c, 32 * wc))) != 0xFu) b += 4;
     }
     if (x == 0) b += 64;  // the fresh L_j+1,j L_j+1,j^T product of the look-ahead
+    if (post) b += POST_BLOCKS;  // (A_ij - acc) Dinv_jj^T
     return b;
   };
   double blocks = 0;
@@ -167,6 +183,7 @@ double panel_even(int T, int n, int j, bool eval) {
   if (nf > 2) blocks += (nf - 2) * factor_wg(1);
   if (eval && j > 0) {
     const bool has_next = j + 1 < T;
+    if (post) blocks += j * POST_BLOCKS;  // -acc Dinv_jj^T, one per W tile
     for (int w = 0; w < 8; ++w) {
       const int wr = (w >> 2) & 1, wc = w & 3;
       const int nlim = ((wc < 2 && j == T - 1) || (wc >= 2 && j + 1 == T - 1)) ? rT : OI_NB;
@@ -181,7 +198,7 @@ double panel_even(int T, int n, int j, bool eval) {
   return blocks * BLK;
 }
 
-double chol_panel(int T, int n, int j, int kbeg, bool eval) {
+double chol_panel(int T, int n, int j, int kbeg, bool eval, bool post) {
   const int rT = n - OI_NB * (T - 1), nf = T - 1 - j;
   auto factor_wg = [&](int x) {
     const int i = j + 1 + x;
@@ -190,10 +207,12 @@ double chol_panel(int T, int n, int j, int kbeg, bool eval) {
       const int wr = w >> 1, wc = w & 1;
       const unsigned s = i == T - 1 ? pad_skip(32 * wr, 32 * wc, OI_NB, rT) : 0u;
       b += 4.0 * (j - kbeg) * live(s);
-      for (int c = 0; c < 4; ++c) b += live(s | rows_above(c, 32 * wr));  // the Dinv_jj pair
+      if (!post)
+        for (int c = 0; c < 4; ++c) b += live(s | rows_above(c, 32 * wr));  // the Dinv_jj pair
       if (x == 0) b += 4.0 * j * live(lower_blocks(32 * wr, 32 * wc));  // look-ahead syrk
     }
     if (x == 0) b += 64;  // its fresh L_ij L_ij^T product
+    if (post) b += POST_BLOCKS;  // Dinv_jj (A_ij^T - acc)
     return b;
   };
   double blocks = 0;
@@ -210,11 +229,13 @@ double chol_panel(int T, int n, int j, int kbeg, bool eval) {
         tri_first += live(s | cols_below(c, 32 * wc));
         dinv_last += live(s | rows_above(c, 32 * wr));
       }
+      if (post) dinv_last = POST_BLOCKS / 4;  // Dinv_jj (Vneg - acc), every W tile (per wave: 4 waves)
       for (int jj = 0; jj < j && jj < kbeg; ++jj)  // extra pair: k = kbeg .. j
         blocks += 4.0 * (j - kbeg) * live(s) + dinv_last;
       // kfirst = jj (jj >= kbeg): pairs k = jj .. j-1, the first against W_jj,jj
       const int lo = kbeg < j ? kbeg : j;
-      for (int jj = lo; jj < j; ++jj) blocks += 4.0 * (j - jj - 1) * live(s) + tri_first;
+      for (int jj = lo; jj < j; ++jj)
+        blocks += 4.0 * (j - jj - 1) * live(s) + tri_first + (post ? dinv_last : 0.0);
     }
   }
   return blocks * BLK;
@@ -446,7 +467,7 @@ struct Slot {
 class Engine {
  public:
   Engine(Context& ctx, const oi_options& o, int64_t cap_hint)
-      : ctx_(ctx), o_(o), legacy_(legacy_panels()) {
+      : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()) {
     HIPC(hipSetDevice(ctx.device));
     st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
     static const bool debug_set = [] {
@@ -823,7 +844,7 @@ class Engine {
       mark(K_CHOL, true);
       const bool even = !legacy_ && (j % 2 == 0);
       const int kbeg = (legacy_ || even) ? 0 : j - 1;
-      if (j > kbeg) {  // P_jk for kbeg <= k < j: nothing to scale at j = 0
+      if (pform_ && j > kbeg) {  // P_jk for kbeg <= k < j: nothing to scale at j = 0
         mark(K_SCALE, false);
         rc |= oi_launch_scale(dc, dl_all, cnt, j, kbeg, gst);
         mark(K_SCALE, true);
@@ -834,24 +855,24 @@ class Engine {
       if (empty_panel) {
       } else if (even) {
         mark(K_EVEN, false);
-        rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
+        rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
         mark(K_EVEN, true);
       } else {
         mark(K_TRSM, false);
-        rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, gst);
+        rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
         mark(K_TRSM, true);
       }
       if (o_.profile) {  // executed MFMA flops, mirroring the kernels' masks (acct::)
         for (int k = 0; k < cnt; ++k) {
           const OiCell& cd = hc(all_slots[k]);
           const bool ev = cd.mode == OI_MODE_EVAL;
-          if (j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
+          if (pform_ && j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
           if (empty_panel)
             continue;
           else if (even)
-            kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev);
+            kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev, !pform_);
           else
-            kfl_[K_TRSM] += acct::chol_panel(cd.T, cd.n, j, kbeg, ev);
+            kfl_[K_TRSM] += acct::chol_panel(cd.T, cd.n, j, kbeg, ev, !pform_);
         }
       }
     }
@@ -988,7 +1009,7 @@ class Engine {
 
   Context& ctx_;
   oi_options o_;
-  bool legacy_ = false, poison_ = false;
+  bool legacy_ = false, pform_ = false, poison_ = false;
   hipStream_t st_ = nullptr;
   hipEvent_t ready_ = nullptr;
   int cap_ = 1, G_ = 1, capG_ = 1;

@@ -840,6 +840,81 @@ __device__ __forceinline__ void alpha_update(const OiCell& c, const double* X, i
 //                k_diag_factor(j+1).
 //   x >= T-1-j : (eval) tile (j, jj = x-(T-1-j)) of W = L^-1:
 //                  W_j,jj = sum_{k=jj}^{j-1} P_jk W_k,jj
+// Post-form (POST, default): the GEMM loop streams L_jk instead of P_jk and the
+// Dinv_jj product is applied once to the finished sum (post_left), so no
+// k_scale launch and no P tiles are needed:
+//   L_ij^T  = Dinv_jj (A_ij^T - sum_{k=kbeg}^{j-1} L_jk L_ik^T)
+//   W_j,jj  = Dinv_jj (Vneg - sum_{k=kfirst}^{j-1} L_jk W_k,jj)   (Vneg = 0 if kfirst = jj)
+// out(m, n) = sum_q Dinv[m][q] S(q, n), S(m, n) = base[m*64 + n] - acc(m, n)
+// (base null: S = -acc).  S is staged in LDS (B operand); Dinv_jj (column-major,
+// lower triangular, zero above the diagonal) is read into registers once, all
+// loads in flight together.  The 160 block-k-steps of the triangular product
+// are split evenly: wave w owns row blocks {0, 3} (w even) or {1, 2} and column
+// blocks 2(w>>1), 2(w>>1)+1 -- 40 MFMAs per wave.  The result is written to
+// dst[m*64 + n] and staged in lds as X[m*XLD + n] (what fwd_update /
+// alpha_update and the look-ahead read).
+__device__ __forceinline__ void post_left(const Quad& acc, double* lds, const double* base, const double* Dj,
+                                          double* dst) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int mA = (w & 1) ? 1 : 0, mB = 3 - mA, n0 = 2 * (w >> 1);
+  double bv[16];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        bv[(2 * mb + nb) * 4 + r] = base ? gld(base + acc1_row(mb, r) * NB + acc1_col(nb)) : 0.0;
+  __syncthreads();  // the GEMM's last LDS reads are done
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)  // B(q, n) = S[q][n] at q*XLD + n
+        lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = bv[(2 * mb + nb) * 4 + r] - acc.c[mb][nb][r];
+  // A(m, q) = Dinv[m][q] at Dj[q*64 + m]: row block mA needs k-steps kk <= 4 mA + 3, mB up to
+  // 4 mB + 3; loaded once S is staged (acc, bv dead: the kernel stays at 4 waves per SIMD)
+  double dA[8], dB[16];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) dA[kk] = kk <= 4 * mA + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * mA + fr) : 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) dB[kk] = kk <= 4 * mB + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * mB + fr) : 0.0;
+  __syncthreads();
+  d4 o[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) o[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const int k = 4 * kk + fk;
+    const double b0 = lds[k * XLD + 16 * n0 + fr], b1 = lds[k * XLD + 16 * n0 + 16 + fr];
+    if (kk <= 4 * mA + 3) {  // wave-uniform
+      o[0][0] = MFMA64(dA[kk < 8 ? kk : 7], b0, o[0][0]);
+      o[0][1] = MFMA64(dA[kk < 8 ? kk : 7], b1, o[0][1]);
+    }
+    if (kk <= 4 * mB + 3) {
+      o[1][0] = MFMA64(dB[kk], b0, o[1][0]);
+      o[1][1] = MFMA64(dB[kk], b1, o[1][1]);
+    }
+  }
+  __syncthreads();  // S is read before the result replaces it
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * (a ? mB : mA) + (lane >> 4) + 4 * r, n = 16 * (n0 + b) + fr;
+        gst(dst + m * NB + n, o[a][b][r]);
+        lds[m * XLD + n] = o[a][b][r];
+      }
+  __syncthreads();
+}
+
+template <bool POST>
 __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ cells,
                                                    const int32_t* __restrict__ list, int j,
                                                    int kbeg, int gx, int ncell) {
@@ -865,31 +940,33 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       b = tileL(c, i, k);  // k == j: A_ij, already holding A_ij - sum_{k<kbeg} L_ik L_jk^T
     };
     const double pre = fwd_preload(c, i, j);
-    const int chD = 4 * (j - kbeg);  // first chunk of the Dinv_jj pair (A(m, k) = 0 for k > m)
-    auto cm = [=](int ch) { return ch >= chD ? rows_above(ch - chD, 32 * wr) : 0u; };
     // n = row of block row i: padding rows of the last block are skipped
-    gemm1_kmajor<true>(acc, lds, 4 * (j + 1 - kbeg), i == T - 1 ? pad_skip(32 * wr, 32 * wc, NB, rT) : 0u,
-                       fpair, cm);
+    const unsigned psk = i == T - 1 ? pad_skip(32 * wr, 32 * wc, NB, rT) : 0u;
     double* Y = tileL(c, i, j);
-    for (int mb = 0; mb < 2; ++mb)
-      for (int nb = 0; nb < 2; ++nb)
-        for (int r = 0; r < 4; ++r) {
-          gst(Y + acc1_row(mb, r) * NB + acc1_col(nb), acc.c[mb][nb][r]);  // L_ij, column-major
-          lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // staged: X[col*XLD + row]
-        }
-    __syncthreads();
+    if constexpr (POST) {
+      gemm1_kmajor<true>(acc, lds, 4 * (j - kbeg), psk, [=, &c](int p, const double*& a, const double*& b) {
+        a = tileL(c, j, kbeg + p);
+        b = tileL(c, i, kbeg + p);
+      });
+      post_left(acc, lds, Y, Dj, Y);  // L_ij^T = Dinv_jj (A_ij^T - acc), stored and staged
+    } else {
+      const int chD = 4 * (j - kbeg);  // first chunk of the Dinv_jj pair (A(m, k) = 0 for k > m)
+      auto cm = [=](int ch) { return ch >= chD ? rows_above(ch - chD, 32 * wr) : 0u; };
+      gemm1_kmajor<true>(acc, lds, 4 * (j + 1 - kbeg), psk, fpair, cm);
+      for (int mb = 0; mb < 2; ++mb)
+        for (int nb = 0; nb < 2; ++nb)
+          for (int r = 0; r < 4; ++r) {
+            gst(Y + acc1_row(mb, r) * NB + acc1_col(nb), acc.c[mb][nb][r]);  // L_ij, column-major
+            lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // staged: X[col*XLD + row]
+          }
+      __syncthreads();
+    }
     fwd_update<256>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) return;
-    __syncthreads();  // the staged tile is read before the look-ahead reuses lds
     // ---- look-ahead: diagonal tile j+1 = i.
     // S_d = A_ii - L_ij L_ij^T - sum_{k<j} L_ik L_ik^T; the first product uses
-    // this workgroup's own L_ij, written k-major (X[c][m] = L_ij[m][c] = acc
-    // entry (c, m)) into LDS.
-    double* Xs = lds;
-    for (int mb = 0; mb < 2; ++mb)
-      for (int nb = 0; nb < 2; ++nb)
-        for (int r = 0; r < 4; ++r) Xs[acc1_row(mb, r) * LDSA + acc1_col(nb)] = acc.c[mb][nb][r];
-    __syncthreads();
+    // this workgroup's own L_ij, staged k-major in lds (X[c*XLD + m] = L_ij[m][c])
+    const double* Xs = lds;
     Quad accd;
     quad_zero(accd);
     {
@@ -898,8 +975,8 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
 #pragma unroll 4
       for (int kk = 0; kk < NB / 4; ++kk) {
         const int k = kk * 4 + fk;
-        const double a0 = Xs[k * LDSA + 32 * wr + fr], a1 = Xs[k * LDSA + 32 * wr + 16 + fr];
-        const double b0 = Xs[k * LDSA + 32 * wc + fr], b1 = Xs[k * LDSA + 32 * wc + 16 + fr];
+        const double a0 = Xs[k * XLD + 32 * wr + fr], a1 = Xs[k * XLD + 32 * wr + 16 + fr];
+        const double b0 = Xs[k * XLD + 32 * wc + fr], b1 = Xs[k * XLD + 32 * wc + 16 + fr];
         accd.c[0][0] = MFMA64(a0, b0, accd.c[0][0]);
         accd.c[0][1] = MFMA64(a0, b1, accd.c[0][1]);
         accd.c[1][0] = MFMA64(a1, b0, accd.c[1][0]);
@@ -934,22 +1011,32 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
     b = tileW(c, k, jj);  // k == j: Vneg
   };
   const double apre = alpha_preload(c, jj, j);
-  // pair k = jj: B = W_jj,jj (B(k, n) = 0 for k < n); pair k = j: A = Dinv_jj
-  const int chD = extra ? 4 * (j - kfirst) : 1 << 30;
-  auto cm = [=](int ch) {
-    return (!extra && ch < 4 ? cols_below(ch, 32 * wc) : 0u) | (ch >= chD ? rows_above(ch - chD, 32 * wr) : 0u);
-  };
   // m = row of W block row j: padding rows of the last block are skipped
-  gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst + extra), j == T - 1 ? pad_skip(32 * wr, 32 * wc, rT, NB) : 0u,
-                     wpair, cm);
+  const unsigned psk = j == T - 1 ? pad_skip(32 * wr, 32 * wc, rT, NB) : 0u;
   double* Wt = tileW(c, j, jj);
-  for (int mb = 0; mb < 2; ++mb)
-    for (int nb = 0; nb < 2; ++nb)
-      for (int r = 0; r < 4; ++r) {
-        gst(Wt + acc1_row(mb, r) * NB + acc1_col(nb), acc.c[mb][nb][r]);  // row-major
-        lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // X[row of W * XLD + col]
-      }
-  __syncthreads();
+  if constexpr (POST) {
+    // pair k = jj: B = W_jj,jj (B(k, n) = 0 for k < n)
+    auto cm = [=](int ch) { return !extra && ch < 4 ? cols_below(ch, 32 * wc) : 0u; };
+    gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst), psk, [=, &c](int p, const double*& a, const double*& b) {
+      a = tileL(c, j, kfirst + p);
+      b = tileW(c, kfirst + p, jj);
+    }, cm);
+    post_left(acc, lds, extra ? Wt : nullptr, Dj, Wt);  // W_j,jj = Dinv_jj (Vneg - acc), stored and staged
+  } else {
+    // pair k = jj: B = W_jj,jj (B(k, n) = 0 for k < n); pair k = j: A = Dinv_jj
+    const int chD = extra ? 4 * (j - kfirst) : 1 << 30;
+    auto cm = [=](int ch) {
+      return (!extra && ch < 4 ? cols_below(ch, 32 * wc) : 0u) | (ch >= chD ? rows_above(ch - chD, 32 * wr) : 0u);
+    };
+    gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst + extra), psk, wpair, cm);
+    for (int mb = 0; mb < 2; ++mb)
+      for (int nb = 0; nb < 2; ++nb)
+        for (int r = 0; r < 4; ++r) {
+          gst(Wt + acc1_row(mb, r) * NB + acc1_col(nb), acc.c[mb][nb][r]);  // row-major
+          lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = acc.c[mb][nb][r];  // X[row of W * XLD + col]
+        }
+    __syncthreads();
+  }
   alpha_update<256>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
 }
 
@@ -995,6 +1082,88 @@ __device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, dou
   }
 }
 
+// dst[n*64 + m] (op)= X[n*XLD + m] for a tile staged in lds (second half of emit_half)
+__device__ __forceinline__ void emit_copy(const double* X, double* dst, int op) {
+  for (int e = threadIdx.x; e < OI_TILE; e += GEMM_THREADS) {
+    const double v = X[(e >> 6) * XLD + (e & 63)];
+    if (op == EMIT_STORE)
+      gst(dst + e, v);
+    else if (op == EMIT_SUB)
+      gst(dst + e, gld(dst + e) - v);
+    else
+      gst(dst + e, -v);
+  }
+}
+
+// Post-form (POST): half 0 accumulates sum_{k<j} L_ik L_jk^T (factor) or
+// sum_k W_k,jj^T L_jk^T (W rows) and is finished by post_right:
+//   L_ij = (A_ij - acc) Dinv_jj^T,   W_j,jj^T = -acc Dinv_jj^T.
+// out(m, n) = sum_q S(m, q) Dinv[n][q], S(m, n) = base[n*64 + m] - acc(m, n)
+// (base null: S = -acc).  S is staged in LDS at X[q*XLD + m] (A operand) and
+// Dinv_jj's ten lower 16x16 blocks next to it, packed (block (I, K) at
+// (I(I+1)/2 + K) * 272, element (n, k) at (k & 15) * 17 + (n & 15)); both
+// global reads are issued before the first barrier.  All eight waves share
+// the 160 block-k-steps of the triangular product: wave w owns row block w & 3
+// and column blocks {0, 3} (w < 4) or {1, 2} -- 20 MFMAs each.  The result is
+// left staged as X[n*XLD + m] (emit_half's layout) for emit_copy.
+#define DPK_OFF (NB * XLD)
+__device__ __forceinline__ void post_right(const Quad& acc, double* lds, const double* base, const double* Dj) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const bool mine = (w & 3) < 2;  // the waves holding half 0
+  double dv[5];                   // 2560 packed Dinv entries, 5 per thread
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int e = t + GEMM_THREADS * q, blk = e >> 8, kl = (e >> 4) & 15, nl = e & 15;
+    const int I = blk >= 6 ? 3 : blk >= 3 ? 2 : blk >= 1 ? 1 : 0, K = blk - I * (I + 1) / 2;
+    dv[q] = gld(Dj + (16 * K + kl) * NB + 16 * I + nl);
+  }
+  double bv[16];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        bv[(2 * mb + nb) * 4 + r] = (mine && base) ? gld(base + acc_col(nb) * NB + acc_row(mb, r)) : 0.0;
+  __syncthreads();  // the GEMM's last LDS reads are done
+  if (mine) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          lds[acc_col(nb) * XLD + acc_row(mb, r)] = bv[(2 * mb + nb) * 4 + r] - acc.c[mb][nb][r];
+  }
+  double* Dp = lds + DPK_OFF;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int e = t + GEMM_THREADS * q, blk = e >> 8, kl = (e >> 4) & 15, nl = e & 15;
+    Dp[blk * 272 + kl * 17 + nl] = dv[q];
+  }
+  __syncthreads();
+  const int mb = w & 3, nA = (w >> 2) ? 1 : 0, nB = 3 - nA;
+  d4 o0 = (d4){0.0, 0.0, 0.0, 0.0}, o1 = o0;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const int k = 4 * kk + fk, K = kk >> 2;
+    const double a = lds[k * XLD + 16 * mb + fr];
+    // B(k, n) = Dinv[n][k]: block (nX, K), zero for K > nX (wave-uniform skip)
+    if (kk <= 4 * nA + 3) o0 = MFMA64(a, Dp[(nA * (nA + 1) / 2 + K) * 272 + (k & 15) * 17 + fr], o0);
+    if (kk <= 4 * nB + 3) o1 = MFMA64(a, Dp[(nB * (nB + 1) / 2 + K) * 272 + (k & 15) * 17 + fr], o1);
+  }
+  __syncthreads();  // S and Dinv are read before the result replaces S
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = 16 * mb + (lane >> 4) + 4 * r;
+    lds[(16 * nA + fr) * XLD + m] = o0[r];
+    lds[(16 * nB + fr) * XLD + m] = o1[r];
+  }
+  __syncthreads();
+}
+
+template <bool POST>
 __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __restrict__ cells,
                                                             const int32_t* __restrict__ list,
                                                             int j, int gx, int ncell) {
@@ -1037,9 +1206,19 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
     const int chD = 4 * j;
     const unsigned sk = pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim) |
                         (x == 0 && wc >= 2 ? upper_blocks(32 * wr, 32 * (wc - 2)) : 0u);
-    auto cm = [=](int ch) { return ch < chD ? 0u : wc >= 2 ? 0xFu : cols_above(ch - chD, 32 * wc); };
-    gemm2_kmajor<true>(acc, lds, j + 1, fpair, sk, cm);
-    emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij (staged in lds as X[col*XLD+row])
+    if constexpr (POST) {
+      gemm2_kmajor<true>(acc, lds, j, [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
+        a = tileL(c, i, p);
+        b0 = tileL(c, j, p);
+        b1 = tileL(c, j + 1, p);
+      }, sk);
+      post_right(acc, lds, tileL(c, i, j), Dj);  // L_ij = (A_ij - acc) Dinv_jj^T, staged
+      emit_copy(lds, tileL(c, i, j), EMIT_STORE);
+    } else {
+      auto cm = [=](int ch) { return ch < chD ? 0u : wc >= 2 ? 0xFu : cols_above(ch - chD, 32 * wc); };
+      gemm2_kmajor<true>(acc, lds, j + 1, fpair, sk, cm);
+      emit_half(acc, 0, lds, tileL(c, i, j), EMIT_STORE);  // L_ij (staged in lds as X[col*XLD+row])
+    }
     fwd_update<GEMM_THREADS>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) {
       emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1
@@ -1073,7 +1252,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   auto wpair = [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
     const int k = jj + p;
     a = tileW(c, k, jj);
-    b0 = Pj + (size_t)k * OI_TILE;
+    b0 = POST ? tileL(c, j, k) : Pj + (size_t)k * OI_TILE;
     b1 = has_next ? tileL(c, j + 1, k) : g_zero_tile;
   };
   // n = row of W block row j (half 0) or j+1 (half 1)
@@ -1083,7 +1262,12 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   const unsigned sk = pad_skip(0, 32 * (wc & 1), NB, nlim) | (!has_next && wc >= 2 ? 0xFu : 0u);
   auto cm = [=](int ch) { return ch < 4 ? rows_below(ch, 32 * wr) : 0u; };
   gemm2_kmajor<true>(acc, lds, j - jj, wpair, sk, cm);
-  emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);           // W_j,jj (row-major), staged X[n*XLD+m]
+  if constexpr (POST) {
+    post_right(acc, lds, nullptr, Dj);  // W_j,jj^T = -acc Dinv_jj^T, staged
+    emit_copy(lds, tileW(c, j, jj), EMIT_STORE);
+  } else {
+    emit_half(acc, 0, lds, tileW(c, j, jj), EMIT_STORE);  // W_j,jj (row-major), staged X[n*XLD+m]
+  }
   alpha_update<GEMM_THREADS>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
   if (has_next) emit_half(acc, 1, lds, tileW(c, j + 1, jj), EMIT_NEG);  // Vneg
 }
@@ -1553,20 +1737,28 @@ extern "C" int oi_launch_scale(const OiCell* cells, const int32_t* list, int nce
 }
 
 extern "C" int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                                    int j, int kbeg, int with_trtri, void* stream) {
+                                    int j, int kbeg, int with_trtri, int pform, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
-  hipLaunchKernelGGL(k_chol_panel, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j,
-                     kbeg, gx, ncell);
+  if (pform)
+    hipLaunchKernelGGL(k_chol_panel<false>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j,
+                       kbeg, gx, ncell);
+  else
+    hipLaunchKernelGGL(k_chol_panel<true>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j,
+                       kbeg, gx, ncell);
   return ret();
 }
 
 extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                                    int j, int with_trtri, void* stream) {
+                                    int j, int with_trtri, int pform, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
-  hipLaunchKernelGGL(k_panel_even, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
-                     list, j, gx, ncell);
+  if (pform)
+    hipLaunchKernelGGL(k_panel_even<false>, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
+                       list, j, gx, ncell);
+  else
+    hipLaunchKernelGGL(k_panel_even<true>, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
+                       list, j, gx, ncell);
   return ret();
 }
 

@@ -186,14 +186,18 @@ def test_panel_schemes_agree(scheme, monkeypatch):
         assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
 
 
-@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4')])
+@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4'), ('OI_PFORM', '1')])
 def test_alternate_kernels_agree(knob, value, monkeypatch):
     """The A/B alternates kept in the library -- round 1's 32-blocked diagonal
-    factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r) and the
-    128x128 K^-1 / gradient kernel (OI_LAUUM=4) -- meet the T1 tolerance on
-    tile-boundary sizes, fit and predict."""
+    factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r), the
+    128x128 K^-1 / gradient kernel (OI_LAUUM=4) and the P-form panels
+    (OI_PFORM=1: k_scale's P_jk = -Dinv_jj L_jk streamed by the panels, both
+    panel schemes) -- meet the T1 tolerance on tile-boundary sizes, fit and
+    predict."""
     monkeypatch.setenv(knob, value)
     test_panel_schemes_agree('2', monkeypatch)
+    if knob == 'OI_PFORM':
+        test_panel_schemes_agree('1', monkeypatch)
 
 
 def test_config5_size_n5000():
