@@ -44,7 +44,7 @@ struct OiCell {
   double* L;          // packed lower tiles (T(T+1)/2 * 4096)
   double* W;          // packed lower tiles of L^-1 (eval mode), else null
   double* Dinv;       // T * 4096
-  double* P;          // T * 4096: P_jk = -Dinv_jj L_jk of the current block column
+  double* P;          // T * 4096: P_jk = -Dinv_jj L_jk of the current block column (P-form only, else null)
   double* vec;        // 4 * T * 64: z | alpha | kstar | v.  z = L^-1 r and (predict)
                       // v = L^-1 k* are built in place during the factorisation
   double* part;       // partial sums, see OI_PART_*

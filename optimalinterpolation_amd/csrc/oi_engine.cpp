@@ -104,14 +104,14 @@ class Arena {
   std::map<size_t, size_t> free_;
 };
 
-size_t cell_bytes(int64_t n, bool eval) {
+size_t cell_bytes(int64_t n, bool eval, bool ptiles) {
   const size_t T = (size_t)tiles_of(n), nt = T * (T + 1) / 2;
   size_t b = 0;
   auto add = [&](size_t x) { b += (x + 255) & ~size_t(255); };
   add(nt * OI_TILE * 8);                         // L
   if (eval) add(nt * OI_TILE * 8);               // W
   add(T * OI_TILE * 8);                          // Dinv
-  add(T * OI_TILE * 8);                          // P
+  if (ptiles) add(T * OI_TILE * 8);              // P (P-form panels only, OI_PFORM=1)
   add(4 * T * OI_NB * 8);                        // vec
   add((size_t)OI_PART_SIZE(nt, T) * 8);          // part
   return b;
@@ -609,7 +609,7 @@ class Engine {
     jb.dw = d_dw;
     size_t max_cell = 0;
     for (int64_t c = 0; c < nc; ++c)
-      max_cell = std::max(max_cell, cell_bytes(jb.m[c], jb.kind != Job::PREDICT_ONLY));
+      max_cell = std::max(max_cell, cell_bytes(jb.m[c], jb.kind != Job::PREDICT_ONLY, pform_));
     if (max_cell > ctx_.arena.size()) {
       ctx_.arena.release(jb.in_off, jb.in_bytes);
       jb.in_off = SIZE_MAX;
@@ -706,7 +706,7 @@ class Engine {
       const Job& job = *jp;
       const int64_t n = job.m[c];  // the cell's problem size: its distinct sites
       const bool eval_mem = job.kind != Job::PREDICT_ONLY;
-      const size_t bytes = cell_bytes(n, eval_mem);
+      const size_t bytes = cell_bytes(n, eval_mem, pform_);
       const size_t off = ctx_.arena.alloc(bytes);
       if (off == SIZE_MAX) break;
       queue_.pop_front();
@@ -733,7 +733,7 @@ class Engine {
       cd.L = take(nt * OI_TILE * 8);
       cd.W = eval_mem ? take(nt * OI_TILE * 8) : nullptr;
       cd.Dinv = take((size_t)T * OI_TILE * 8);
-      cd.P = take((size_t)T * OI_TILE * 8);
+      cd.P = pform_ ? take((size_t)T * OI_TILE * 8) : nullptr;
       cd.vec = take(4 * (size_t)T * OI_NB * 8);
       cd.part = take((size_t)OI_PART_SIZE(nt, T) * 8);
       cd.xyt = job.sites + 3 * job.offs[c];

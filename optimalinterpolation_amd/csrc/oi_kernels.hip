@@ -182,8 +182,22 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
     }
   }
   double* Y = tileL(c, i, j);
-  for (int e = t; e < OI_TILE; e += 256) {
-    int r = e & 63, cc = e >> 6, a = i * NB + r, b = j * NB + cc;
+  // a diagonal tile is built on its lower triangle only (2080 entries, column-
+  // packed so whole waves retire early): the factor kernels treat the upper
+  // triangle as scratch and clear it (k_diag_factor*)
+  const int ne = i == j ? NB * (NB + 1) / 2 : OI_TILE;
+  for (int e = t; e < ne; e += 256) {
+    int r, cc;
+    if (i == j) {  // column cc starts at S(cc) = 64 cc - cc (cc - 1) / 2
+      cc = (int)((129.0 - sqrt(16641.0 - 8.0 * e)) * 0.5);
+      while (cc > 0 && NB * cc - cc * (cc - 1) / 2 > e) --cc;
+      while (NB * (cc + 1) - (cc + 1) * cc / 2 <= e) ++cc;
+      r = cc + (e - (NB * cc - cc * (cc - 1) / 2));
+    } else {
+      r = e & 63;
+      cc = e >> 6;
+    }
+    const int a = i * NB + r, b = j * NB + cc;
     double val;
     if (a >= n || b >= n) {
       val = (a == b) ? 1.0 : 0.0;
@@ -193,7 +207,7 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
       val = (dws[0][r] * dws[1][cc]) * (sf2 * ((1.0 + Q) * exp(-Q)));  // M = D Kd D (+ sn2 I)
       if (a == b) val += sn2;
     }
-    gst(Y + e, val);
+    gst(Y + cc * NB + r, val);
   }
 }
 
