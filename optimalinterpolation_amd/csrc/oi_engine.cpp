@@ -316,6 +316,7 @@ std::vector<std::pair<std::string, ExtStat>> g_ext;
 struct Context {
   int device = 0;
   hipStream_t own_stream = nullptr;
+  hipStream_t sub_stream = nullptr;  // submissions (residuals, sites): never behind a round in flight
   std::vector<hipStream_t> aux;  // extra streams for concurrent cell groups
   hipStream_t aux_stream(int g) {
     while ((int)aux.size() < g) {
@@ -342,6 +343,7 @@ Context& context(int device, int64_t pool_bytes) {
     p->device = device;
     HIPC(hipSetDevice(device));
     HIPC(hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking));
+    HIPC(hipStreamCreateWithFlags(&p->sub_stream, hipStreamNonBlocking));
   }
   HIPC(hipSetDevice(device));
   size_t want = (size_t)pool_bytes;
@@ -470,6 +472,7 @@ class Engine {
       : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()) {
     HIPC(hipSetDevice(ctx.device));
     st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
+    ss_ = ctx.sub_stream;
     static const bool debug_set = [] {
       const char* e = getenv("OI_DEBUG");
       if (e && atoi(e) == 1) oi_set_debug(1);
@@ -545,7 +548,13 @@ class Engine {
     if (o_.device_inputs && N > 0) {
       HIPC(hipEventRecord(ready_, o_.stream ? (hipStream_t)o_.stream : (hipStream_t)0));
       for (Group& gr : groups_) HIPC(hipStreamWaitEvent(gr.st, ready_, 0));
+      HIPC(hipStreamWaitEvent(ss_, ready_, 0));
     }
+    // The submission's own work (residuals, copies, k_dedup, the m / SSW
+    // read-back) runs on the submit stream: the host waits for it alone, not
+    // for the round in flight on the group streams (a session's submit used to
+    // drain the GPU once per batch).  Arena blocks are released only after the
+    // rounds that used them completed, so the new block never overlaps them.
     // one block: residuals | sites | v | d | offs | m | SSW (| host inputs' copy)
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
     const size_t N1 = (size_t)std::max<int64_t>(N, 1), C1 = (size_t)std::max<int64_t>(nc, 1);
@@ -576,7 +585,7 @@ class Engine {
     double* d_ssw = (double*)take(sz[6]);
     const double* d_x = xyt_in;
     if (o_.device_inputs) {
-      if (N > 0 && oi_launch_residual(y, mX, jb.mean, d_r, N, st_))
+      if (N > 0 && oi_launch_residual(y, mX, jb.mean, d_r, N, ss_))
         throw HipError("residual kernel launch failed");
     } else {
       double* dx = (double*)take(sz[7]);
@@ -584,8 +593,8 @@ class Engine {
       if (N > 0) {
         jb.r_host.resize(N);
         for (int64_t a = 0; a < N; ++a) jb.r_host[a] = y[a] - (mX ? mX[a] : 1.0 * jb.mean);
-        HIPC(hipMemcpyAsync(dx, xyt_in, N * 3 * 8, hipMemcpyHostToDevice, st_));
-        HIPC(hipMemcpyAsync(d_r, jb.r_host.data(), N * 8, hipMemcpyHostToDevice, st_));
+        HIPC(hipMemcpyAsync(dx, xyt_in, N * 3 * 8, hipMemcpyHostToDevice, ss_));
+        HIPC(hipMemcpyAsync(d_r, jb.r_host.data(), N * 8, hipMemcpyHostToDevice, ss_));
       }
     }
     // distinct sites of every cell; the host needs m to size and order cells
@@ -594,14 +603,14 @@ class Engine {
     if (nc > 0) {
       int64_t maxn = 0;
       for (int64_t c = 0; c < nc; ++c) maxn = std::max(maxn, jb.offs[c + 1] - jb.offs[c]);
-      HIPC(hipMemcpyAsync(d_offs, jb.offs.data(), (nc + 1) * 8, hipMemcpyHostToDevice, st_));
+      HIPC(hipMemcpyAsync(d_offs, jb.offs.data(), (nc + 1) * 8, hipMemcpyHostToDevice, ss_));
       if (oi_launch_dedup(d_x, d_r, d_offs, (int)nc, (int)std::min<int64_t>(maxn, INT32_MAX),
-                          dedup_enabled() ? 0 : 1, d_sites, d_v, d_dw, d_m, d_ssw, st_))
+                          dedup_enabled() ? 0 : 1, d_sites, d_v, d_dw, d_m, d_ssw, ss_))
         throw HipError(std::string("dedup kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-      HIPC(hipMemcpyAsync(jb.m.data(), d_m, nc * 4, hipMemcpyDeviceToHost, st_));
-      HIPC(hipMemcpyAsync(jb.ssw.data(), d_ssw, nc * 8, hipMemcpyDeviceToHost, st_));
+      HIPC(hipMemcpyAsync(jb.m.data(), d_m, nc * 4, hipMemcpyDeviceToHost, ss_));
+      HIPC(hipMemcpyAsync(jb.ssw.data(), d_ssw, nc * 8, hipMemcpyDeviceToHost, ss_));
     }
-    HIPC(hipStreamSynchronize(st_));  // m known; host inputs may be released on return
+    HIPC(hipStreamSynchronize(ss_));  // m known; host inputs may be released on return
     jb.xyt = d_x;
     jb.r = d_r;
     jb.sites = d_sites;
@@ -616,11 +625,8 @@ class Engine {
       throw NoMem("a cell needs " + std::to_string(max_cell) + " bytes of workspace, pool is " +
                   std::to_string(ctx_.arena.size()));
     }
-    if (G_ > 1) {  // the other groups' streams see the inputs
-      HIPC(hipEventRecord(ready_, st_));
-      for (Group& gr : groups_)
-        if (gr.st != st_) HIPC(hipStreamWaitEvent(gr.st, ready_, 0));
-    }
+    // (the submission completed on the host's clock: every group stream's later
+    // launches see its outputs)
     // admission order inside the batch: largest cells first (cost ~ m^3), ties by index
     std::vector<int64_t> order(nc);
     std::iota(order.begin(), order.end(), 0);
@@ -1010,7 +1016,7 @@ class Engine {
   Context& ctx_;
   oi_options o_;
   bool legacy_ = false, pform_ = false, poison_ = false;
-  hipStream_t st_ = nullptr;
+  hipStream_t st_ = nullptr, ss_ = nullptr;
   hipEvent_t ready_ = nullptr;
   int cap_ = 1, G_ = 1, capG_ = 1;
   std::vector<Slot> slots_;
