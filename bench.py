@@ -817,6 +817,9 @@ def main():
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and not opt:
         workers, desc = host_cores(args)
         line["cpu_baseline"] = cpu_predict_baseline(workers, desc)
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and single:
+        workers, desc = host_cores(args)
+        line["cpu_baseline"] = cpu_single_baseline([args.seed + 31 * k for k in range(done_k)], workers, desc)
     else:
         line["cpu_baseline"] = None
     if rank == 0:
@@ -827,6 +830,22 @@ def main():
                 f.write(s + '\n')
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_single_baseline(seeds, workers, desc):
+    """Config 1 on the CPU: the oracle's full GPR3D(opt=True) (GPR:143-191 with
+    scipy's CG) on the same n = 200 cells the GPU leg timed, each fit in its
+    own single-threaded-BLAS process (one cell per MPI rank in the reference);
+    the latency metric is one cell at a time, so value = 1 / mean fit time on
+    one core (the fits run ``workers`` at a time only to finish sooner)."""
+    res = run_jobs([('fit', 200, sd) for sd in seeds], workers, time.time() + 120)
+    if not res:
+        return {"value": None, "error": "no CPU fit finished"}
+    t = float(np.mean([r['fit_s'] for r in res]))
+    return {"value": 1.0 / t, "unit": "grid-cells/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/gp_oracle.py GPR3D(opt=True) on the {len(res)} timed n=200 cells, one "
+                       f"single-threaded-BLAS process per cell, mean fit {t * 1e3:.1f} ms, "
+                       f"{float(np.mean([r['evals'] for r in res])):.1f} evaluations/cell ({desc})")}
 
 
 def cpu_predict_baseline(workers, desc):
