@@ -51,6 +51,7 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 matrix (= vector) dense peak, spec
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
 METRIC = "grid-cells/sec (full GP fit+predict), 25 km pan-Arctic day, fp64"
 X0 = np.array([np.log(25e3), np.log(25e3), 0.0, 0.0, 0.0, np.log(.1)])  # GPR:217
+X0_12P5 = np.array([np.log(12.5e3), np.log(12.5e3), 0.0, 0.0, 0.0, np.log(.1)])  # GPR:217, grid_res = 12.5
 
 
 def parse():
@@ -58,7 +59,11 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=2)
-    p.add_argument('--workload', default='day', choices=['day', 'days', 'predict', 'single', 'nystrom', 'svgp'])
+    p.add_argument('--workload', default='day',
+                   choices=['day', 'days', 'season', 'predict', 'single', 'nystrom', 'svgp'])
+    p.add_argument('--season-shares', type=int, default=8,
+                   help='season workload: the 12.5 km day is LPT-split into this many GPU shares; rank r '
+                        'fits share r (config 5 = 8 shares on 8 GPUs; at N = 1 one 1/8 share)')
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--slices', default='ordered', choices=['lpt', 'ordered'],
                    help='day slices: equal-cost LPT mixes (lpt) or consecutive runs of the '
@@ -78,6 +83,10 @@ def parse():
     p.add_argument('--timed-profile', default='auto', choices=['auto', 'on', 'off'],
                    help='per-launch HIP events inside the timed region (auto: on for day/days; off for '
                         'single/predict, whose roofline then comes from a second, profiled pass)')
+    p.add_argument('--parity-cells', type=int, default=24,
+                   help='day workloads: timed cells re-checked against the CPU oracle at the GPU fit\'s '
+                        'hypers (T1, SURVEY §8c), stratified over n; 0 = skip')
+    p.add_argument('--dump', default='', help='write per-cell n, m, evals, status of the timed cells (.npz)')
     p.add_argument('--out', default='')
     return p.parse_args()
 
@@ -112,11 +121,11 @@ def host_cores(args=None):
 
 
 # ----------------------------------------------------------------- workloads
-def split_slices(sizes, k, how='lpt'):
+def split_slices(sizes, k, how='lpt', sites=None):
     """Cell index sets of ``k`` slices of equal estimated cost (driver.cell_costs)."""
     from optimalinterpolation_amd import driver
     k = max(1, min(int(k), len(sizes))) if len(sizes) else 1
-    costs = driver.cell_costs(sizes)
+    costs = driver.cell_costs(sizes, sites=sites)
     if how == 'lpt':
         return driver.lpt_partition(costs, k)
     order = np.argsort(-np.asarray(sizes), kind='stable')  # the engine's admission order
@@ -131,29 +140,48 @@ def build_slices(args, rank, world):
     from optimalinterpolation_amd import driver, synthetic
     warm = [synthetic.make_cells(np.random.default_rng(900 + g).integers(300, 1201, 24),
                                  seed=1000 + 97 * g + rank) for g in range(args.warmup)]
+    if args.workload == 'season':
+        shares = max(int(args.season_shares), world)
+        cen, sizes = synthetic.season_day_plan(seed=args.seed)
+        est = driver.expected_sites(sizes, grid_m=synthetic.GRID_12P5_M)
+        parts = driver.lpt_partition(driver.cell_costs(sizes, sites=est), shares)
+        mine = synthetic.season_cells(cen, sizes, parts[rank], seed=args.seed)
+        cfg = {"workload": (f"config 5: one day of the 12.5 km season (640x640 grid, {len(sizes)} cells, "
+                            f"n ~ U{{300..5000}}), opt=True fit+predict; LPT-split into {shares} GPU shares, "
+                            f"this run fits {world} of them (share r on rank r), one slice per step"),
+               "day_cells": int(len(sizes)), "n_obs_per_cell": "U{300..5000}", "grid_km": 12.5,
+               "x0": "GPR_CS2S3.py:217 with grid_res = 12.5", "shares": shares,
+               "cells_total": int(sum(len(parts[r]) for r in range(world))), "cells_per_rank": int(mine.ncell),
+               "parallelism": f"dp{world} ({shares}-way LPT partition on E(n) m^3, m = expected sites)"}
+        sites = driver.site_counts(mine)
+        sl = split_slices(mine.sizes, args.steps, args.slices, sites)
+        return ([mine.subset(s) for s in sl], warm, True, cfg, "weak",
+                [len(parts[r]) for r in range(world)])
     if args.workload in ('day', 'days'):
         seed = args.seed + (rank if args.workload == 'days' else 0)
         day = synthetic.make_day(seed=seed)
         common = {"day_cells": int(day.ncell), "n_obs_per_cell": "U{300..3000}", "grid_km": 25,
                   "x0": "GPR_CS2S3.py:217", "slices": args.slices}
+        day_sites = driver.site_counts(day)
         if args.workload == 'day':
-            parts = driver.lpt_partition(driver.cell_costs(day.sizes), world)
+            parts = driver.lpt_partition(driver.cell_costs(day.sizes, sites=day_sites), world)
             mine = day.subset(parts[rank])
+            mine_sites = day_sites[parts[rank]]
             cfg = {"workload": ("25km pan-Arctic day, opt=True fit+predict per cell "
                                 f"(config {'3' if world == 1 else '4'}: the whole day on {world} GPU"
                                 f"{'s' if world > 1 else ''}, one slice per step)"),
                    **common, "cells_total": int(day.ncell), "cells_per_rank": int(mine.ncell),
-                   "parallelism": f"dp{world} (LPT cell partition, one RCCL gather)"}
+                   "parallelism": f"dp{world} (LPT cell partition on E(n) m^3, one RCCL gather)"}
             scaling = "strong"
             counts_all = [len(p) for p in parts]
         else:
-            mine = day
+            mine, mine_sites = day, day_sites
             cfg = {"workload": "one synthetic 25km day per rank (seed + rank), opt=True fit+predict, "
                                "one slice per step", **common, "cells_total": int(day.ncell) * world,
                    "parallelism": f"dp{world} (a day per GPU, one RCCL gather)"}
             scaling = "weak"
             counts_all = [int(day.ncell)] * world  # day_centres() is the same grid for every seed
-        sl = split_slices(mine.sizes, args.steps, args.slices)
+        sl = split_slices(mine.sizes, args.steps, args.slices, mine_sites)
         return [mine.subset(s) for s in sl], warm, True, cfg, scaling, counts_all
     if args.workload == 'predict':
         cells = [synthetic.make_cells([500] * 1000, seed=args.seed + 7919 * k + rank) for k in range(args.steps)]
@@ -667,6 +695,7 @@ def main():
     from optimalinterpolation_amd import _lib, synthetic
 
     slices, warm, opt, cfg, scaling, counts_all = build_slices(args, rank, world)
+    x0 = X0_12P5 if args.workload == 'season' else X0
     log(f"rank {rank}: {len(slices)} slices, {sum(s.ncell for s in slices)} cells")
 
     def resident(cells):  # inputs in HBM before timing
@@ -679,7 +708,7 @@ def main():
 
     def submit(sess, item):
         cells, xyt, z, h = item
-        return sess.submit(xyt, z, cells.offs, cells.xs, cells.mean, x0=X0 if opt else None, opt=opt, hyp=h)
+        return sess.submit(xyt, z, cells.offs, cells.xs, cells.mean, x0=x0 if opt else None, opt=opt, hyp=h)
 
     # library initialisation (context, arena, code objects): one untimed
     # one-shot call on 8 small cells -- not a step
@@ -727,12 +756,12 @@ def main():
     # the single gather of posterior fields (ncell x 8 fp64) to rank 0
     rows = np.concatenate([outs[k][0] for k in range(done_k)]) if done_k else np.zeros((0, 8))
     if world > 1:
-        if truncated:  # per-rank counts then differ from the partition's: exchange them
-            cs = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
-            dist.all_gather(cs, torch.tensor([rows.shape[0]], dtype=torch.int64, device=cdev))
-            kmax = int(max(int(c.item()) for c in cs))
-        else:  # known on every rank from the (deterministic) partition
-            kmax = int(max(counts_all))
+        # every rank takes the same collective path: the row counts are always
+        # exchanged (one tiny all_gather), since a rank that hit --budget-s on
+        # its own clock holds fewer rows than the partition gave it
+        cs = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
+        dist.all_gather(cs, torch.tensor([rows.shape[0]], dtype=torch.int64, device=cdev))
+        kmax = int(max(int(c.item()) for c in cs))
         pay = torch.zeros((max(kmax, 1), 8), dtype=torch.float64, device=cdev)
         pay[:rows.shape[0]] = torch.from_numpy(rows).to(cdev)
         bufs = [torch.empty_like(pay) for _ in range(world)] if rank == 0 else None
@@ -773,7 +802,10 @@ def main():
     sites_timed = np.concatenate([site_counts(slices[k]) for k in range(done_k)])
     evals = info[:, 3].astype(float) if opt else np.zeros(len(sizes_timed))
     n = sites_timed.astype(float)
-    line = {"metric": METRIC if args.workload in ('day', 'days') else f"grid-cells/sec ({args.workload}), fp64",
+    metric = (METRIC if args.workload in ('day', 'days') else
+              "grid-cells/sec (full GP fit+predict), 12.5 km season day, fp64" if args.workload == 'season' else
+              f"grid-cells/sec ({args.workload}), fp64")
+    line = {"metric": metric,
             "value": round(total_cells / dt, 4), "unit": "grid-cells/s", "n_gpus": world,
             "steps": done_k, "warmup": args.warmup, "ms_per_step": round(dt / max(done_k, 1) * 1e3, 3),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f64",
@@ -802,10 +834,24 @@ def main():
                 "rocprofv3 --kernel-trace --stats run of this command averages over"}
     if done_k != args.steps or truncated:
         line.update({"truncated": True, "steps_requested": args.steps})
+    if args.dump:
+        np.savez(args.dump if rank == 0 else f"{args.dump}.rank{rank}.npz", n=sizes_timed, m=sites_timed,
+                 evals=info[:, 3], nit=info[:, 0], cg_status=info[:, 1], status=status)
     if rank == 0:
         log("line (before cpu_baseline): " + json.dumps({k: line[k] for k in ('value', 'steps', 'ms_per_step')}))
+    if rank == 0 and opt and args.parity_cells > 0 and args.workload in ('day', 'days', 'season'):
+        try:
+            timed = [slices[k] for k in range(done_k)]
+            rows = np.concatenate([outs[k][0] for k in range(done_k)])
+            line["parity"] = timed_parity(timed, rows, status, args.parity_cells, gpu,
+                                          T_PROC + args.budget_s + 10.0, host_cores(args)[0])
+        except Exception as e:  # never lose the GPU line over the check
+            line["parity"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and opt and args.workload != 'single':
         workers, desc = host_cores(args)
+        if args.workload == 'season':
+            global EVAL_PROBES
+            EVAL_PROBES = (300, 1000, 2000, 3000, 4000, 5000)
         deadline = T_PROC + args.budget_s + 20.0
         if time.time() + 30 > deadline:
             line["cpu_baseline"] = {"value": None, "error": "skipped: wall-clock budget spent by the GPU leg"}
@@ -830,6 +876,108 @@ def main():
                 f.write(s + '\n')
     if world > 1:
         dist.destroy_process_group()
+
+
+CHECK_JOB = r'''
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from oracle import gp_oracle as O
+d = np.load(sys.argv[2])
+x, y, xs, mean, hyp = d['x'], d['y'], d['xs'], float(d['mean']), d['hyp']
+h = np.r_[np.log(hyp), np.log(.1)]
+f, g = O.neg_log_ml(h, x, y, np.ones(len(y)) * mean)
+fs, sd, lz = O.predict(x, y, xs, mean, hyp[:3], hyp[3], hyp[4])
+# S_j = 1/2 sum |Q o dK_j|: the magnitude of what the gradient sums (tests/test_gpu_parity.py)
+n = len(y)
+K, dK = O.matern32(x, hyp[:3], hyp[3], grad=True)
+Kinv = np.linalg.inv(K + np.eye(n) * hyp[4])
+a = Kinv @ (y - mean)
+Q = Kinv - np.outer(a, a)
+S = [np.abs(Q * dK[j]).sum() / 2 for j in range(3)] + [np.abs(Q * 2 * K).sum() / 2,
+                                                      hyp[4] * np.abs(np.diag(Q)).sum(), 0.0]
+print(json.dumps({"nlz": float(np.asarray(f).ravel()[0]), "grad": [float(v) for v in np.ravel(g)],
+                  "gscale": [float(v) for v in S],
+                  "fs": float(np.ravel(fs)[0]), "sd": float(np.ravel(sd)[0]), "lz": float(np.ravel(lz)[0])}))
+'''
+
+
+def timed_parity(timed, rows, status, k, gpu, deadline, workers):
+    """T1 parity of the bench's own timed cells (SURVEY §8c): a stratified
+    sample of ``k`` timed cells (equal-count n buckets, spread inside each),
+    the GPU's objective (oi_nlml_grad_batch, SMLII GPR:107-141) and the fitted
+    cells' posterior (fs, sd, lZ: the timed run's own output rows, GPR:173-182)
+    against the CPU oracle (bit-exact restatement of GPR:78-191) at the hypers
+    the GPU fit found.  Tolerance 1e-10 relative (max(1, |ref|)); the gradient
+    as |dg| <= 1e-10 (|g| + S_j), S_j = 1/2 sum |Q o dK_j| (tests/test_gpu_parity.py)."""
+    import tempfile
+    from optimalinterpolation_amd import _lib, synthetic
+    cells = [(t, c) for t in timed for c in range(t.ncell)]
+    sizes = np.array([t.offs[c + 1] - t.offs[c] for t, c in cells])
+    ok = np.flatnonzero(status == 0)
+    order = ok[np.argsort(sizes[ok], kind='stable')]
+    pick = [int(b[len(b) // 2]) for b in np.array_split(order, min(k, len(order))) if len(b)]
+    sub = synthetic.RaggedCells(np.concatenate([cells[p][0].cell(cells[p][1])[0] for p in pick]),
+                                np.concatenate([cells[p][0].cell(cells[p][1])[1] for p in pick]),
+                                np.concatenate([[0], np.cumsum(sizes[pick])]),
+                                np.concatenate([cells[p][0].cell(cells[p][1])[2] for p in pick]),
+                                timed[0].mean)
+    hyp = rows[pick, 3:8]
+    h6 = np.column_stack([np.log(hyp), np.full(len(pick), np.log(.1))])
+    nlz, grad, st = _lib.nlml_grad_batch(sub.xyt, sub.z, np.full(len(sub.z), sub.mean), sub.offs, h6, device=gpu)
+    tmp = tempfile.mkdtemp(prefix='oi_parity_')
+    jobs = []
+    for q in range(len(pick)):
+        x, y, xs = sub.cell(q)
+        path = os.path.join(tmp, f'c{q}.npz')
+        np.savez(path, x=x, y=y, xs=xs, mean=sub.mean, hyp=hyp[q])
+        jobs.append([path])
+    res = run_argv_jobs(CHECK_JOB, jobs, workers, deadline)
+    rel = lambda a, b: abs(a - b) / max(1.0, abs(b))
+    worst = {"nlz": 0.0, "grad": 0.0, "fs": 0.0, "sd": 0.0, "lz": 0.0}
+    checked = 0
+    for q, r in enumerate(res):
+        if r is None:
+            continue
+        checked += 1
+        worst["nlz"] = max(worst["nlz"], rel(nlz[q], r["nlz"]))
+        g = np.array(r["grad"])
+        sc = np.maximum(np.abs(g) + np.array(r["gscale"]), 1e-300)
+        worst["grad"] = max(worst["grad"], float(np.max(np.abs(grad[q] - g) / sc)))
+        for key, col in (("fs", 0), ("sd", 1), ("lz", 2)):
+            worst[key] = max(worst[key], rel(rows[pick[q], col], r[key]))
+    n_chk = [int(sizes[pick[q]]) for q in range(len(pick)) if res[q] is not None]
+    return {"cells": checked, "n_min": min(n_chk) if n_chk else None, "n_max": max(n_chk) if n_chk else None,
+            "max_rel_nlz": worst["nlz"], "max_rel_grad": worst["grad"], "max_rel_fs": worst["fs"],
+            "max_rel_sd": worst["sd"], "max_rel_lz": worst["lz"], "tol": 1e-10,
+            "pass": bool(checked == len(pick) and max(worst.values()) <= 1e-10 and np.all(st == 0)),
+            "note": ("T1 at the GPU fit's hypers: the timed run's fs/sd/lZ rows and oi_nlml_grad_batch's nlZ/"
+                     "gradient vs oracle/gp_oracle.py (n x n, duplicate sites included) on a stratified sample "
+                     "of the timed cells, CPU processes on the host after the timed region")}
+
+
+def run_argv_jobs(script, jobs, workers, deadline):
+    """``script`` in single-threaded-BLAS subprocesses, one per argument list in
+    ``jobs`` (``workers`` at a time); -> parsed JSON per job (None if it failed
+    or was not started before ``deadline``)."""
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    res = [None] * len(jobs)
+    pending, running = list(range(len(jobs))), []
+    while pending or running:
+        while pending and len(running) < workers and time.time() < deadline:
+            q = pending.pop(0)
+            running.append((q, subprocess.Popen([sys.executable, '-c', script, ROOT] + [str(a) for a in jobs[q]],
+                                                stdout=subprocess.PIPE, text=True, env=env)))
+        if pending and time.time() >= deadline:
+            pending = []
+        for q, p in list(running):
+            if p.poll() is not None:
+                out = p.stdout.read()
+                running.remove((q, p))
+                if p.returncode == 0 and out.strip():
+                    res[q] = json.loads(out.strip().splitlines()[-1])
+        time.sleep(0.05)
+    return res
 
 
 def cpu_single_baseline(seeds, workers, desc):

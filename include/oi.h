@@ -95,6 +95,10 @@ int oi_gpr_batch(const double* xyt, const double* z, const int64_t* offs, int64_
  *   oi_session_wait    runs rounds until the ticket completes (ticket < 0: all
  *                      submitted work); it may return with later batches'
  *                      rounds still in flight on the device.
+ *   oi_session_set_stream  the stream whose queued work later submissions'
+ *                      DEVICE inputs are ordered after (default: opts->stream
+ *                      at creation, NULL = the legacy NULL stream); the
+ *                      session's rounds keep running on their own stream.
  *   oi_session_done    1 if the ticket has completed, else 0.
  *   oi_session_destroy waits for in-flight rounds and frees the session
  *                      (unfinished cells are dropped, outputs left unwritten).
@@ -105,6 +109,7 @@ int64_t oi_session_submit(oi_session* s, const double* xyt, const double* z, con
                           int64_t ncell, const double* xs, double mean, const double* x0,
                           int32_t opt, const double* hyp, double* out, int32_t* status,
                           int32_t* info);
+int oi_session_set_stream(oi_session* s, void* stream);
 int oi_session_wait(oi_session* s, int64_t ticket);
 int oi_session_done(oi_session* s, int64_t ticket);
 void oi_session_destroy(oi_session* s);

@@ -36,7 +36,8 @@ EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_cr
            'oi_version', 'oi_profile_json', 'oi_profile_reset', 'oi_smooth_fields',
            'oi_ball_query', 'oi_gather_rows', 'oi_nystrom_batch',
            'oi_nystrom_fit_batch', 'oi_svgp_batch', 'oi_svgp_param_count', 'oi_session_create',
-           'oi_session_submit', 'oi_session_wait', 'oi_session_done', 'oi_session_destroy')
+           'oi_session_submit', 'oi_session_set_stream', 'oi_session_wait', 'oi_session_done',
+           'oi_session_destroy')
 
 
 class OiOptions(ctypes.Structure):
@@ -124,6 +125,8 @@ def load():
                                           ctypes.c_int64, c_double_p, ctypes.c_double, c_double_p,
                                           ctypes.c_int32, c_double_p, c_double_p, c_int32_p, c_int32_p]
         lib.oi_session_submit.restype = ctypes.c_int64
+        lib.oi_session_set_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        lib.oi_session_set_stream.restype = ctypes.c_int
         lib.oi_session_wait.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         lib.oi_session_wait.restype = ctypes.c_int
         lib.oi_session_done.argtypes = [ctypes.c_void_p, ctypes.c_int64]
@@ -256,7 +259,12 @@ class Session:
     ``wait(ticket)`` returns that batch's (out, status, info) once complete,
     leaving later batches' rounds running on the GPU.  Cells of consecutive
     batches share rounds, so a stream of small batches runs at the rate of one
-    big call; per-cell results equal oi_gpr_batch's bit for bit."""
+    big call; per-cell results equal oi_gpr_batch's bit for bit.
+
+    Device inputs are ordered after torch's current stream AT EACH SUBMIT
+    (oi_session_set_stream), so a producer running under another
+    ``torch.cuda.stream(...)`` context is waited for.  Results of a ticket are
+    collected once: by ``wait(ticket)``, or in the dict ``wait()`` returns."""
 
     def __init__(self, device=0, device_inputs=False, **opt_kw):
         self._lib = load()
@@ -268,7 +276,8 @@ class Session:
         self._h = self._lib.oi_session_create(ctypes.byref(self._opts))
         if not self._h:
             raise OiError(f"oi_session_create: {self._lib.oi_last_error().decode(errors='replace')}")
-        self._live = {}
+        self._live = {}    # ticket -> results (and the inputs they keep alive), not yet complete
+        self._done = {}    # ticket -> results completed by wait(-1), not yet collected
 
     def submit(self, xyt, z, offs, xs, mean, x0=None, opt=True, hyp=None):
         offs = np.ascontiguousarray(offs, dtype=np.int64)
@@ -281,6 +290,7 @@ class Session:
             _check_dev(xyt, self.device, n=3 * N, what='xyt')
             _check_dev(z, self.device, n=N, what='z')
             px, pz = _dptr(xyt), _dptr(z)
+            _check(self._lib.oi_session_set_stream(self._h, _caller_stream(self.device)))
         else:
             xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
             z = np.ascontiguousarray(z, dtype=np.float64)
@@ -311,13 +321,23 @@ class Session:
         return self._lib.oi_session_done(self._h, int(ticket)) == 1
 
     def wait(self, ticket=-1):
-        """Block until ``ticket`` completes (all work when -1); returns its
-        (out, status, info), or None for ticket -1."""
-        _check(self._lib.oi_session_wait(self._h, int(ticket)))
+        """Block until ``ticket`` completes and return its (out, status, info).
+        ``ticket = -1`` drains all submitted work and returns
+        ``{ticket: (out, status, info)}`` for every ticket not collected yet
+        (those can still be collected one by one with ``wait(ticket)``)."""
+        ticket = int(ticket)
+        if ticket >= 0:
+            if ticket in self._done:
+                return self._done.pop(ticket)
+            if ticket not in self._live:
+                raise KeyError(f"unknown or already collected session ticket {ticket}")
+        _check(self._lib.oi_session_wait(self._h, ticket))
         if ticket < 0:
+            for t, (out, status, info, _, _) in self._live.items():
+                self._done[t] = (out, status, info)
             self._live.clear()
-            return None
-        out, status, info, _, _ = self._live.pop(int(ticket))
+            return dict(self._done)
+        out, status, info, _, _ = self._live.pop(ticket)
         return out, status, info
 
     def close(self):
@@ -325,6 +345,7 @@ class Session:
             self._lib.oi_session_destroy(self._h)
             self._h = None
             self._live.clear()
+            self._done.clear()
 
     def __enter__(self):
         return self

@@ -21,6 +21,17 @@ enum OiMode { OI_MODE_EVAL = 0, OI_MODE_PREDICT = 1 };
 
 // per-cell status bits (device-written)
 enum OiStatus { OI_OK = 0, OI_NOT_PD = 1 };
+// Duplicate sites and the reference's non-PD branch (GPR:126, :139-140): with
+// repeated rows, numpy's n x n Cholesky of K + sn2 I loses the repeated row's
+// pivot (exact value ~2 sn2) to rounding once sn2 / sf2 falls below a band that
+// grows with n.  Measured on the reference's own cholesky (numpy 2.2.6 /
+// OpenBLAS 0.3.29) over synthetic day cells and permutations of them: failure
+// probability 50 % at sn2 / sf2 ~ 1e-18 n_obs (n = 500: 42 % at 5e-16;
+// n = 1000: 83 % at 1e-15; n = 2000: 50 % at 2e-15), 100 % below a fifth of
+// that and 0 % above 5x (tests/test_gpu_parity.py::test_duplicate_nonpd_band).
+// The m x m site form stays PD, so k_build flags the cell not-PD below the
+// 50 % point (and whenever sf2 + sn2 rounds to sf2).
+#define OI_DUP_NONPD_TAU 1e-18
 
 // Duplicate sites.  Observations with identical (x, y, t) (several
 // satellites binned into one grid cell on one day) give identical rows of K.

@@ -82,6 +82,9 @@ class Arena {
   }
   void release(size_t off, size_t bytes) {
     bytes = (bytes + 255) & ~size_t(255);
+    // a block the arena never handed out (SIZE_MAX = a failed alloc) must not
+    // enter the free list: it would alias live allocations after wrap-around
+    if (off >= size_ || bytes > size_ - off) return;
     auto it = free_.emplace(off, bytes).first;
     auto nx = std::next(it);
     if (nx != free_.end() && it->first + it->second == nx->first) {
@@ -620,7 +623,9 @@ class Engine {
     for (int64_t c = 0; c < nc; ++c)
       max_cell = std::max(max_cell, cell_bytes(jb.m[c], jb.kind != Job::PREDICT_ONLY, pform_));
     if (max_cell > ctx_.arena.size()) {
-      ctx_.arena.release(jb.in_off, jb.in_bytes);
+      // in_off == SIZE_MAX: the inputs went to the job's own buffer, nothing
+      // of the arena to return
+      if (jb.in_off != SIZE_MAX) ctx_.arena.release(jb.in_off, jb.in_bytes);
       jb.in_off = SIZE_MAX;
       throw NoMem("a cell needs " + std::to_string(max_cell) + " bytes of workspace, pool is " +
                   std::to_string(ctx_.arena.size()));
@@ -643,6 +648,10 @@ class Engine {
   }
 
   bool done(int64_t id) const { return id < next_id_ && !jobs_.count(id); }
+
+  // The stream later submissions' device inputs are ordered after (the rounds
+  // keep the stream chosen at construction).
+  void set_input_stream(void* stream) { o_.stream = stream; }
 
   // Drive rounds until batch `id` (or every batch, id < 0) is complete.
   void wait(int64_t id) {
@@ -1204,6 +1213,13 @@ int64_t oi_session_submit(oi_session* s, const double* xyt, const double* z, con
   } catch (const std::bad_alloc&) {
     return fail(OI_E_NOMEM, "host allocation failed");
   }
+}
+
+int oi_session_set_stream(oi_session* s, void* stream) {
+  if (!s) return fail(OI_E_ARG, "null session");
+  std::lock_guard<std::mutex> lk(s->ctx->mu);
+  s->eng->set_input_stream(stream);
+  return 0;
 }
 
 int oi_session_wait(oi_session* s, int64_t ticket) {

@@ -158,9 +158,12 @@ __global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
   const double sf2 = c.hyp[3], sn2 = c.hyp[4];
   // Duplicate sites make K + sn2 I singular up to sn2: the reference's
   // n x n Cholesky loses the pivot of a repeated row, (sf2 + sn2) - sf2^2 /
-  // (sf2 + sn2), once sf2 + sn2 rounds to sf2 (sn2 = 0 included) and takes
-  // the LinAlgError branch (GPR:139-140); the m x m site form would not notice.
-  if (x == 0 && t == 0 && c.n_obs > n && sf2 + sn2 == sf2) *c.status = OI_NOT_PD;
+  // (sf2 + sn2), to rounding (always once sf2 + sn2 rounds to sf2, sn2 = 0
+  // included; with probability 1/2 at sn2 / sf2 = OI_DUP_NONPD_TAU n_obs) and
+  // takes the LinAlgError branch (GPR:139-140); the m x m site form would not
+  // notice (oi_device.h).
+  if (x == 0 && t == 0 && c.n_obs > n && (sf2 + sn2 == sf2 || sn2 < OI_DUP_NONPD_TAU * c.n_obs * sf2))
+    *c.status = OI_NOT_PD;
   if (i == j && t < NB) {
     // right-hand sides of the forward substitution run inside the
     // factorisation: z = r (site residuals), and for predict v = k* = D kd*

@@ -141,10 +141,20 @@ def save(dic, path):
         pickle.dump(dic, f, protocol=2)
 
 
-def write_quicklook(path, fs, sd, x=None, y=None, lat=None, lon=None):
-    """The quick-look product layout (``QuickLook Data/*.nc``: radar_freeboard,
-    uncertainty on the 320x320 grid, plus lat/lon) as classic netCDF-3
-    (scipy.io; the HDF5-based netCDF-4 writer is not in this image)."""
+def write_quicklook(path, fs, sd, x=None, y=None, lat=None, lon=None, date='', fmt='netcdf4', created=None):
+    """The quick-look product (``QuickLook Data/CS2S3_<date>_25km_quicklook.nc``:
+    lat, lon, radar_freeboard, uncertainty on the 320 x 320 grid, fp64).
+
+    ``fmt='netcdf4'`` (default) writes the reference's own netCDF-4 / HDF5
+    layout with the from-scratch writer of ``hdf5nc`` (dimensions lat / lon,
+    dimension scales, the reference's attributes); lat / lon default to the
+    grid coordinates ``x`` / ``y`` when no geographic grid is given.
+    ``fmt='netcdf3'`` keeps the classic netCDF-3 file (scipy.io) of round 2."""
+    if fmt == 'netcdf4':
+        from . import hdf5nc
+        lat = np.asarray(lat if lat is not None else (x if x is not None else np.zeros_like(fs)), dtype=np.float64)
+        lon = np.asarray(lon if lon is not None else (y if y is not None else np.zeros_like(fs)), dtype=np.float64)
+        return hdf5nc.write_quicklook(path, fs, sd, lat, lon, date=date or '00000000', created=created)
     from scipy.io import netcdf_file
     nx, ny = fs.shape
     with netcdf_file(path, 'w') as f:
@@ -156,6 +166,7 @@ def write_quicklook(path, fs, sd, x=None, y=None, lat=None, lon=None):
                 continue
             v = f.createVariable(name, 'f8', ('x', 'y'))
             v[:] = np.asarray(arr, dtype=np.float64)
+    return path
 
 
 class DayResult(dict):

@@ -3,8 +3,8 @@
 The reference distributes cells round-robin over MPI ranks
 (``split``, GPR_CS2S3.py:18-23; ``COMM.scatter`` :256) and gathers the
 per-cell tuples back to rank 0 (``COMM.gather`` :262).  Here: one process per
-GPU; cells are partitioned by longest-processing-time-first on an n^3 cost
-estimate (or the reference's strided split); every rank runs its cells through
+GPU; cells are partitioned by longest-processing-time-first on an E(n) m^3 cost
+estimate (m = distinct sites, the size of the problem actually solved) (or the reference's strided split); every rank runs its cells through
 one batched liboi call; the ncell x 8 fp64 results come back to rank 0 in one
 collective -- a single ``gather`` (every rank computes the same partition, so
 no size exchange is needed), RCCL over xGMI on GPUs, gloo in CPU tests.  There is no other
@@ -31,13 +31,45 @@ def lpt_partition(costs, world):
     return [np.array(sorted(p), dtype=np.int64) for p in parts]
 
 
-def cell_costs(sizes, opt=True):
-    """Relative cost model: opt cells ~ E(n) * n^3 with E(n) ~ 85 + 0.045 (n - 300)
-    (SURVEY.md §6 fit); predict-only cells ~ n^3 / 3."""
+def site_counts(cells):
+    """Distinct (x, y, t) sites per cell: the size m of the m x m problem the
+    library solves for a cell of n observations (oi_device.h "Duplicate
+    sites"; DESIGN.md §3b)."""
+    v = np.ascontiguousarray(cells.xyt).view(np.dtype((np.void, 24))).ravel()
+    return np.array([len(np.unique(v[a:b])) for a, b in zip(cells.offs[:-1], cells.offs[1:])], dtype=np.int64)
+
+
+def expected_sites(sizes, grid_m=25e3, radius_m=300e3, t_days=9):
+    """Expected distinct sites of n observations drawn uniformly over the
+    lattice nodes of a radius_m disc x t_days days (the synthetic generator,
+    SURVEY §8d): S (1 - exp(-n / S)), S = nodes x days.  Used to balance cells
+    whose observations a rank has not drawn yet (config 5)."""
     n = np.asarray(sizes, dtype=np.float64)
+    S = np.pi * (radius_m / grid_m) ** 2 * t_days
+    return S * -np.expm1(-n / S)
+
+
+# E(n): SMLII evaluations per opt=True cell.  Refitted on the build's own day
+# run (bench.py --dump: info[:, 3] of the 9997 timed cells, round 3), linear in n
+EVALS_A, EVALS_B = 85.0, 0.045
+
+
+def evals_model(sizes):
+    n = np.asarray(sizes, dtype=np.float64)
+    return EVALS_A + EVALS_B * np.maximum(n - 300.0, 0.0)
+
+
+def cell_costs(sizes, opt=True, sites=None):
+    """Relative cost model for partitioning cells.  The work of a cell is done
+    on its m distinct sites (``sites``; default: ``sizes``, i.e. m = n):
+    opt cells E(n) (m^3 + 40 m^2), the SMLII evaluations times the potrf +
+    trtri + lauum work per evaluation (SURVEY §8d F_eval); predict-only cells
+    m^3 / 3."""
+    n = np.asarray(sizes, dtype=np.float64)
+    m = n if sites is None else np.asarray(sites, dtype=np.float64)
     if not opt:
-        return n ** 3 / 3 + 1.0
-    return (85.0 + 0.045 * np.maximum(n - 300.0, 0.0)) * (n ** 3 + 40 * n ** 2) + 1.0
+        return m ** 3 / 3 + 16 * m ** 2 + 1.0
+    return evals_model(n) * (m ** 3 + 40 * m ** 2) + 1.0
 
 
 def gather_rows(local_rows, parts, ncell, device=None, group=None, to_all=False):
@@ -80,17 +112,21 @@ def gather_rows(local_rows, parts, ncell, device=None, group=None, to_all=False)
     return full
 
 
-def run_sharded(cells, compute, rank, world, device=None, partition='lpt', opt=True, group=None):
+def run_sharded(cells, compute, rank, world, device=None, partition='lpt', opt=True, group=None,
+                sites=None):
     """Pass 1 over a day on ``world`` ranks.
 
     ``cells``   synthetic.RaggedCells-like (all ranks hold the same metadata)
     ``compute`` callable(subset_cells) -> (out [k x 8], status [k], info [k x 4])
                 (the product passes the liboi batched call; CPU tests pass a stub)
+    ``sites``   distinct sites per cell for the cost model (default: counted)
     Returns (full ncell x 13 array on rank 0: out | status | info, else None).
     """
     sizes = cells.sizes
     if partition == 'lpt':
-        parts = lpt_partition(cell_costs(sizes, opt), world)
+        if sites is None:
+            sites = site_counts(cells)
+        parts = lpt_partition(cell_costs(sizes, opt, sites), world)
     else:
         parts = strided_partition(cells.ncell, world)
     mine = parts[rank]

@@ -82,8 +82,9 @@ class RaggedCells:
         return RaggedCells(xyt, zz, np.array(offs), self.xs[idx], self.mean)
 
 
-def make_cells(sizes, seed=0, centres=None, mean=PRIOR_MEAN):
-    """Independent synthetic cells with the given obs counts."""
+def make_cells(sizes, seed=0, centres=None, mean=PRIOR_MEAN, grid_m=GRID_M):
+    """Independent synthetic cells with the given obs counts (observation
+    sites snapped to a ``grid_m`` lattice, as binned satellite data are)."""
     rng = np.random.default_rng(seed)
     sizes = np.asarray(sizes, dtype=np.int64)
     if centres is None:
@@ -91,7 +92,7 @@ def make_cells(sizes, seed=0, centres=None, mean=PRIOR_MEAN):
         centres = cen[rng.integers(0, len(cen), len(sizes))]
     xs_all, zs_all, offs = [], [], [0]
     for (cx, cy), n in zip(centres, sizes):
-        x, z = cell_obs(rng, cx, cy, int(n))
+        x, z = cell_obs(rng, cx, cy, int(n), grid_m=grid_m)
         xs_all.append(x)
         zs_all.append(z)
         offs.append(offs[-1] + int(n))
@@ -110,6 +111,36 @@ def make_day(seed=0, n_lo=300, n_hi=3000, radius_m=1410e3, max_cells=None):
         cen = cen[:max_cells]
     sizes = rng.integers(n_lo, n_hi + 1, len(cen))
     return make_cells(sizes, seed=seed + 1, centres=cen)
+
+
+GRID_12P5_M = 12.5e3
+
+
+def season_day_plan(seed=0, n_lo=300, n_hi=5000, radius_m=1410e3):
+    """Config 5, one day of the season: the 12.5 km grid (640 x 640 over the
+    same [0, 8e6]^2 m domain, GPR_CS2S3.py:201-203 with grid_res = 12.5), ~4e4
+    cell centres inside the disc, n ~ U{n_lo..n_hi}.  Returns
+    (centres [ncell x 2], sizes [ncell]) -- the observations of a cell are
+    drawn by ``season_cells`` only for the cells a rank owns."""
+    rng = np.random.default_rng(seed)
+    cen = day_centres(radius_m, grid_m=GRID_12P5_M)
+    sizes = rng.integers(n_lo, n_hi + 1, len(cen))
+    return cen, sizes
+
+
+def season_cells(centres, sizes, idx, seed=0):
+    """The cells ``idx`` of a season day: each cell's observations from its
+    own stream (seed, cell index), snapped to the 12.5 km lattice, so a rank
+    can draw its share without drawing the whole day."""
+    parts = [make_cells([int(sizes[c])], seed=(seed, int(c)), centres=centres[c:c + 1], grid_m=GRID_12P5_M)
+             for c in np.asarray(idx, dtype=np.int64)]
+    if not parts:
+        return make_cells([], seed=seed)
+    xyt = np.concatenate([p.xyt for p in parts])
+    z = np.concatenate([p.z for p in parts])
+    offs = np.concatenate([[0], np.cumsum([len(p.z) for p in parts])])
+    xs = np.concatenate([p.xs for p in parts])
+    return RaggedCells(xyt, z, offs, xs, parts[0].mean)
 
 
 class BinnedDay:

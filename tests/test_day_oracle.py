@@ -150,7 +150,7 @@ def test_quicklook_writer(tmp_path):
     from scipy.io import netcdf_file
     fs = np.arange(12.0).reshape(3, 4)
     p = str(tmp_path / 'q.nc')
-    day.write_quicklook(p, fs, fs * 0.1, lat=fs + 60, lon=fs - 10)
+    day.write_quicklook(p, fs, fs * 0.1, lat=fs + 60, lon=fs - 10, fmt='netcdf3')
     with netcdf_file(p, 'r', mmap=False) as f:
         assert np.array_equal(f.variables['radar_freeboard'][:], fs)
         assert set(f.variables) == {'lat', 'lon', 'radar_freeboard', 'uncertainty'}

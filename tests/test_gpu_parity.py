@@ -270,3 +270,44 @@ def test_duplicate_sites_reduction():
             assert np.all(np.abs(grad[c, :5] - g[:5]) <= RTOL * (np.abs(g[:5]) + S[:5])), (mode, c, grad[c], g)
             assert close(out[c, 0], fs[0])[0] and close(out[c, 1], sd[0])[0] and close(out[c, 2], lZ)[0], \
                 (mode, c, out[c, :3], fs, sd, lZ)
+
+
+def test_duplicate_nonpd_band():
+    """Duplicate sites at tiny sn2 / sf2 (oi_device.h OI_DUP_NONPD_TAU): the
+    reference's n x n Cholesky (GPR:126) fails on a repeated row's pivot below
+    a band ~max(1e-18 n_obs, 1e-16) that its own rounding decides (permuting the
+    observations moves it); outside [tau / 5, 5 tau] the GPU's status and the
+    oracle's inf / finite SMLII (GPR:139-140) must agree exactly, inside it
+    either outcome is the reference's own noise.  Cells of the synthetic
+    generator (natural lattice duplicates) and two-copy cells, n = 50 .. 1000."""
+    rng = np.random.default_rng(17)
+    sf2 = 4e-3
+    ratios = [1e-17, 1e-16, 3e-16, 1e-15, 3e-15, 1e-14, 1e-13, 1e-12]
+    cases = []
+    for n in (50, 500, 1000):
+        nat = synthetic.make_cells([n], seed=900 + n)
+        x, z, _ = nat.cell(0)
+        cases.append((x, z))
+        idx = rng.permutation(np.repeat(np.arange(n // 2), 2))
+        cases.append((x[:n // 2][idx], z[:n // 2][idx] + rng.normal(0, 0.01, len(idx))))
+    xs, zs, offs, hs, meta = [], [], [0], [], []
+    for x, z in cases:
+        for r in ratios:
+            xs.append(x)
+            zs.append(z)
+            offs.append(offs[-1] + len(z))
+            hs.append([np.log(3e5), np.log(2.5e5), np.log(8.), np.log(sf2), np.log(sf2 * r), 0.0])
+            meta.append((len(z), r))
+    xyt, zz, offs, h = np.concatenate(xs), np.concatenate(zs), np.array(offs), np.array(hs)
+    nlz, grad, st = _lib.nlml_grad_batch(xyt, zz, np.full(len(zz), 0.28), offs, h)
+    disagree_outside, inband = [], []
+    for c, (n, r) in enumerate(meta):
+        x, y = xyt[offs[c]:offs[c + 1]], zz[offs[c]:offs[c + 1]]
+        f, _ = O.neg_log_ml(h[c], x, y, np.ones(n) * 0.28)
+        ref_fail = not np.isfinite(np.ravel(f)[0])
+        gpu_fail = st[c] == 1
+        assert gpu_fail == (not np.isfinite(nlz[c]))
+        tau = max(1e-18 * n, 1e-16)   # small n: the sf2 + sn2 == sf2 rounding rule
+        if gpu_fail != ref_fail:
+            (inband if tau / 5 <= r <= 5 * tau else disagree_outside).append((n, r, ref_fail, gpu_fail))
+    assert not disagree_outside, (disagree_outside, inband)

@@ -97,3 +97,73 @@ def test_device_input_checks():
     with pytest.raises(ValueError, match='cuda'):
         _lib.gpr_batch_device(torch.from_numpy(cells.xyt), torch.from_numpy(cells.z).cuda(),
                               cells.offs, cells.xs, cells.mean, x0=X0)
+
+
+def test_session_wait_all_keeps_results():
+    """wait(-1) drains everything and hands back every uncollected ticket's
+    results; they can still be collected one by one afterwards, once."""
+    cells = synthetic.make_cells([80, 150, 40, 210], seed=53)
+    hyp = np.tile(synthetic.FIXED_HYPERS, (cells.ncell, 1))
+    ref, _, _ = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+    parts = _slices(cells, 2)
+    with _lib.Session() as s:
+        t = [s.submit(p.xyt, p.z, p.offs, p.xs, p.mean, opt=False,
+                      hyp=np.tile(synthetic.FIXED_HYPERS, (p.ncell, 1))) for p in parts]
+        got0 = s.wait(t[0])
+        allres = s.wait(-1)
+        assert set(allres) == {t[1]}
+        got1 = s.wait(t[1])
+        assert got1[0] is allres[t[1]][0]
+        with pytest.raises(KeyError):
+            s.wait(t[1])   # already collected
+        with pytest.raises(KeyError):
+            s.wait(t[0])
+    assert np.array_equal(np.concatenate([got0[0], got1[0]]), ref)
+
+
+def test_session_device_inputs_from_side_stream():
+    """A producer on a non-default torch stream: each submit is ordered after
+    the stream current AT SUBMIT (oi_session_set_stream), not the one current
+    when the session was created."""
+    import torch
+    cells = synthetic.make_cells([300, 120, 450], seed=59)
+    hyp = np.tile(synthetic.FIXED_HYPERS, (cells.ncell, 1))
+    ref, _, _ = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+    xh = torch.from_numpy(cells.xyt).pin_memory()
+    zh = torch.from_numpy(cells.z).pin_memory()
+    side = torch.cuda.Stream()
+    with _lib.Session(device_inputs=True) as s:
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(20_000_000)             # keep the producer stream busy
+            xd = torch.empty_like(xh, device='cuda')
+            zd = torch.empty_like(zh, device='cuda')
+            xd.copy_(xh, non_blocking=True)
+            zd.copy_(zh, non_blocking=True)
+            t = s.submit(xd, zd, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+        out, st, _ = s.wait(t)
+    assert np.array_equal(out, ref)
+
+
+def test_tiny_pool_nomem_then_normal_call():
+    """A batch whose inputs do not fit the arena (they go to a private
+    buffer) and whose cell exceeds it: OI_E_NOMEM, and the arena stays
+    consistent -- the next call with the same pool is bitwise the default's
+    (oi_engine.cpp Engine::submit; ADVICE r2)."""
+    rng = np.random.default_rng(61)
+    ncell, n = 200, 1500                         # 300 k obs: ~22 MB of inputs > 16 MB pool
+    xyt = np.column_stack([rng.uniform(0, 5e5, ncell * n), rng.uniform(0, 5e5, ncell * n),
+                           rng.integers(0, 9, ncell * n).astype(float)])
+    z = rng.normal(0.3, 0.05, ncell * n)
+    offs = np.arange(ncell + 1, dtype=np.int64) * n
+    xs = np.tile([2.5e5, 2.5e5, 4.0], (ncell, 1))
+    pool = 16 << 20
+    with pytest.raises(_lib.OiError, match='-3'):
+        _lib.gpr_batch(xyt, z, offs, xs, 0.28, x0=X0, opt=True, pool_bytes=pool)
+    small = synthetic.make_cells([90, 30, 150, 60], seed=67)
+    hyp = np.tile(synthetic.FIXED_HYPERS, (small.ncell, 1))
+    for _ in range(3):
+        got, st, _ = _lib.gpr_batch(small.xyt, small.z, small.offs, small.xs, small.mean, opt=False, hyp=hyp,
+                                    pool_bytes=pool)
+        assert np.all(st == 0)
+    ref, _, _ = _lib.gpr_batch(small.xyt, small.z, small.offs, small.xs, small.mean, opt=False, hyp=hyp)
+    assert np.array_equal(got, ref)
