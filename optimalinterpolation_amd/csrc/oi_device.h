@@ -97,6 +97,8 @@ int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j, 
 // the GEMM loop); 0 (default): post-form, Dinv_jj applied to the finished sum
 int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
                          int kbeg, int with_trtri, int pform, void* stream);
+int oi_launch_panel4(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j, int with_trtri,
+                     void* stream);
 int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
                          int with_trtri, int pform, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,

@@ -145,6 +145,13 @@ bool pform_panels() {
   const char* e = getenv("OI_PFORM");
   return e && atoi(e) == 1;
 }
+// Even-column panel core, read per call from OI_PANEL4: 1 => k_panel4 (two
+// block rows per workgroup on the 128 x 128 gemm4 core), 0 => k_panel_even
+// (64 x 128 gemm2 core).  Post-form only.
+bool panel4_enabled() {
+  const char* e = getenv("OI_PANEL4");
+  return e && atoi(e) == 1;
+}
 // Executed MFMA flops per cell and launch (profile mode), mirroring the
 // kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
 // 16-deep k-chunk is 8192 flops.  gemm2 (k_panel_even: 8 waves, wr 0..1,
@@ -198,6 +205,44 @@ double panel_even(int T, int n, int j, bool eval, bool post) {
       blocks += 16.0 * (j * (j - 1) / 2.0) + j * first;
     }
   }
+  return blocks * BLK;
+}
+
+// k_panel4 (gemm4: 8 waves of 2 x 4 blocks; per-MFMA masks when `masked`)
+inline int live8(unsigned m) { return __builtin_popcount(~m & 0xFFu); }
+double panel4(int T, int n, int j, bool eval) {
+  const int rT = n - OI_NB * (T - 1), nfp = (T - j) >> 1;
+  double blocks = 0;
+  for (int x = 0; x < nfp; ++x) {
+    const int i1 = j + 1 + 2 * x, i2 = i1 + 1;
+    const bool masked = x == 0 || i2 >= T - 1 || j + 1 == T - 1;
+    for (int w = 0; w < 8; ++w) {
+      const int wr = w >> 1, wc = w & 1, ti = wr >= 2 ? i2 : i1, tj = wc ? j + 1 : j;
+      unsigned skip = 0;
+      for (int mb = 0; mb < 2; ++mb)
+        for (int nb = 0; nb < 4; ++nb) {
+          const int m0 = 32 * (wr & 1) + 16 * mb, n0 = 16 * nb;
+          if (ti >= T || (ti == T - 1 && m0 >= rT) || (tj == T - 1 && n0 >= rT) ||
+              (x == 0 && wr < 2 && wc == 1 && m0 + 15 < n0))
+            skip |= 1u << (4 * mb + nb);
+        }
+      blocks += 4.0 * j * (masked ? live8(skip) : 8);
+    }
+    blocks += POST_BLOCKS * (i2 < T ? 2 : 1);
+    if (x == 0) blocks += 40;  // the look-ahead's 10 lower blocks x 16 MFMAs
+  }
+  if (eval)
+    for (int y = 0; 2 * y < j; ++y) {
+      const bool masked = j >= T - 2;
+      for (int w = 0; w < 8; ++w) {
+        const int wc = w & 1, tj = wc ? j + 1 : j;
+        unsigned skip = 0;
+        for (int nb = 0; nb < 4; ++nb)
+          if ((wc == 1 && j + 1 >= T) || (tj == T - 1 && 16 * nb >= rT)) skip |= 0x11u << nb;
+        blocks += 4.0 * (j - 2 * y) * (masked ? live8(skip) : 8);
+      }
+      blocks += 2 * POST_BLOCKS;
+    }
   return blocks * BLK;
 }
 
@@ -472,7 +517,7 @@ struct Slot {
 class Engine {
  public:
   Engine(Context& ctx, const oi_options& o, int64_t cap_hint)
-      : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()) {
+      : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()), panel4_(panel4_enabled()) {
     HIPC(hipSetDevice(ctx.device));
     st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
     ss_ = ctx.sub_stream;
@@ -870,7 +915,10 @@ class Engine {
       if (empty_panel) {
       } else if (even) {
         mark(K_EVEN, false);
-        rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
+        if (panel4_ && !pform_)
+          rc |= oi_launch_panel4(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
+        else
+          rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
         mark(K_EVEN, true);
       } else {
         mark(K_TRSM, false);
@@ -884,6 +932,8 @@ class Engine {
           if (pform_ && j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
           if (empty_panel)
             continue;
+          else if (even && panel4_ && !pform_)
+            kfl_[K_EVEN] += acct::panel4(cd.T, cd.n, j, ev);
           else if (even)
             kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev, !pform_);
           else
@@ -1024,7 +1074,7 @@ class Engine {
 
   Context& ctx_;
   oi_options o_;
-  bool legacy_ = false, pform_ = false, poison_ = false;
+  bool legacy_ = false, pform_ = false, poison_ = false, panel4_ = false;
   hipStream_t st_ = nullptr, ss_ = nullptr;
   hipEvent_t ready_ = nullptr;
   int cap_ = 1, G_ = 1, capG_ = 1;

@@ -863,7 +863,8 @@ __device__ __forceinline__ void alpha_update(const OiCell& c, const double* X, i
 //   L_ij^T  = Dinv_jj (A_ij^T - sum_{k=kbeg}^{j-1} L_jk L_ik^T)
 //   W_j,jj  = Dinv_jj (Vneg - sum_{k=kfirst}^{j-1} L_jk W_k,jj)   (Vneg = 0 if kfirst = jj)
 // out(m, n) = sum_q Dinv[m][q] S(q, n), S(m, n) = base[m*64 + n] - acc(m, n)
-// (base null: S = -acc).  S is staged in LDS (B operand); Dinv_jj (column-major,
+// (base null: S = -acc).  S is staged in LDS at row stride LDSA = 80 (B operand:
+// rows k, k+1 of a 32-lane ds_read_b64 in opposite bank halves); Dinv_jj (column-major,
 // lower triangular, zero above the diagonal) is read into registers once, all
 // loads in flight together.  The 160 block-k-steps of the triangular product
 // are split evenly: wave w owns row blocks {0, 3} (w even) or {1, 2} and column
@@ -889,8 +890,8 @@ __device__ __forceinline__ void post_left(const Quad& acc, double* lds, const do
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)  // B(q, n) = S[q][n] at q*XLD + n
-        lds[acc1_row(mb, r) * XLD + acc1_col(nb)] = bv[(2 * mb + nb) * 4 + r] - acc.c[mb][nb][r];
+      for (int r = 0; r < 4; ++r)  // B(q, n) = S[q][n] at q*LDSA + n
+        lds[acc1_row(mb, r) * LDSA + acc1_col(nb)] = bv[(2 * mb + nb) * 4 + r] - acc.c[mb][nb][r];
   // A(m, q) = Dinv[m][q] at Dj[q*64 + m]: row block mA needs k-steps kk <= 4 mA + 3, mB up to
   // 4 mB + 3; loaded once S is staged (acc, bv dead: the kernel stays at 4 waves per SIMD)
   double dA[8], dB[16];
@@ -907,7 +908,7 @@ __device__ __forceinline__ void post_left(const Quad& acc, double* lds, const do
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
     const int k = 4 * kk + fk;
-    const double b0 = lds[k * XLD + 16 * n0 + fr], b1 = lds[k * XLD + 16 * n0 + 16 + fr];
+    const double b0 = lds[k * LDSA + 16 * n0 + fr], b1 = lds[k * LDSA + 16 * n0 + 16 + fr];
     if (kk <= 4 * mA + 3) {  // wave-uniform
       o[0][0] = MFMA64(dA[kk < 8 ? kk : 7], b0, o[0][0]);
       o[0][1] = MFMA64(dA[kk < 8 ? kk : 7], b1, o[0][1]);
@@ -1116,14 +1117,21 @@ __device__ __forceinline__ void emit_copy(const double* X, double* dst, int op) 
 // sum_k W_k,jj^T L_jk^T (W rows) and is finished by post_right:
 //   L_ij = (A_ij - acc) Dinv_jj^T,   W_j,jj^T = -acc Dinv_jj^T.
 // out(m, n) = sum_q S(m, q) Dinv[n][q], S(m, n) = base[n*64 + m] - acc(m, n)
-// (base null: S = -acc).  S is staged in LDS at X[q*XLD + m] (A operand) and
-// Dinv_jj's ten lower 16x16 blocks next to it, packed (block (I, K) at
-// (I(I+1)/2 + K) * 272, element (n, k) at (k & 15) * 17 + (n & 15)); both
-// global reads are issued before the first barrier.  All eight waves share
+// (base null: S = -acc).  S is staged in LDS row-major at S[m*SLD + q] (A
+// operand, SLD = 66: the ds_read_b64 of rows k, k+1 by one 32-lane group land
+// on disjoint banks, 4m + 2k mod 64, and the accumulator write-back is 16
+// consecutive doubles per lane group) and Dinv_jj's ten lower 16x16 blocks
+// next to it, packed (block (I, K) at (I(I+1)/2 + K) * 256, element (n, k) at
+// (k & 15) * 16 + (n & 15): rows k, k+1 in opposite bank halves); both global
+// reads are issued before the first barrier.  (Round 2 staged S as X[q*65 + m]
+// and packed Dinv at stride 17: 2-way conflicts on every read, PMC
+// SQ_LDS_BANK_CONFLICT 1.2e11 over the day.)  All eight waves share
 // the 160 block-k-steps of the triangular product: wave w owns row block w & 3
 // and column blocks {0, 3} (w < 4) or {1, 2} -- 20 MFMAs each.  The result is
 // left staged as X[n*XLD + m] (emit_half's layout) for emit_copy.
-#define DPK_OFF (NB * XLD)
+#define SLD 66
+#define DPK_OFF (NB * SLD)
+static_assert(DPK_OFF + 10 * 256 <= GEMM2_LDS, "post_right staging must fit the GEMM LDS");
 __device__ __forceinline__ void post_right(const Quad& acc, double* lds, const double* base, const double* Dj) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
@@ -1151,13 +1159,13 @@ __device__ __forceinline__ void post_right(const Quad& acc, double* lds, const d
       for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          lds[acc_col(nb) * XLD + acc_row(mb, r)] = bv[(2 * mb + nb) * 4 + r] - acc.c[mb][nb][r];
+          lds[acc_row(mb, r) * SLD + acc_col(nb)] = bv[(2 * mb + nb) * 4 + r] - acc.c[mb][nb][r];
   }
   double* Dp = lds + DPK_OFF;
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const int e = t + GEMM_THREADS * q, blk = e >> 8, kl = (e >> 4) & 15, nl = e & 15;
-    Dp[blk * 272 + kl * 17 + nl] = dv[q];
+    Dp[blk * 256 + kl * 16 + nl] = dv[q];
   }
   __syncthreads();
   const int mb = w & 3, nA = (w >> 2) ? 1 : 0, nB = 3 - nA;
@@ -1165,10 +1173,10 @@ __device__ __forceinline__ void post_right(const Quad& acc, double* lds, const d
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
     const int k = 4 * kk + fk, K = kk >> 2;
-    const double a = lds[k * XLD + 16 * mb + fr];
+    const double a = lds[(16 * mb + fr) * SLD + k];
     // B(k, n) = Dinv[n][k]: block (nX, K), zero for K > nX (wave-uniform skip)
-    if (kk <= 4 * nA + 3) o0 = MFMA64(a, Dp[(nA * (nA + 1) / 2 + K) * 272 + (k & 15) * 17 + fr], o0);
-    if (kk <= 4 * nB + 3) o1 = MFMA64(a, Dp[(nB * (nB + 1) / 2 + K) * 272 + (k & 15) * 17 + fr], o1);
+    if (kk <= 4 * nA + 3) o0 = MFMA64(a, Dp[(nA * (nA + 1) / 2 + K) * 256 + (k & 15) * 16 + fr], o0);
+    if (kk <= 4 * nB + 3) o1 = MFMA64(a, Dp[(nB * (nB + 1) / 2 + K) * 256 + (k & 15) * 16 + fr], o1);
   }
   __syncthreads();  // S and Dinv are read before the result replaces S
 #pragma unroll
@@ -1287,6 +1295,248 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
   }
   alpha_update<GEMM_THREADS>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
   if (has_next) emit_half(acc, 1, lds, tileW(c, j + 1, jj), EMIT_NEG);  // Vneg
+}
+
+// --------------------------------------------------- k_panel4(j), j even
+// k_panel_even on the 128 x 128 gemm4 core (OI_PANEL4=1): a workgroup owns TWO
+// block rows, so every streamed tile feeds four outputs instead of two -- half
+// the operand traffic per flop of the 64 x 128 core, whose in-kernel rate
+// (53.9 TF/s executed on the day) sits at its own streaming limit (52.5 TF/s,
+// tools/gemm4_probe.hip; the 128 x 128 core streams at 61).  Slots of a cell:
+//   x <  nfp = ceil((T-1-j)/2) : rows i1 = j+1+2x, i2 = i1+1 (absent past T-1):
+//        quadrant (r, 0) = L_{i_r, j} (post-form: (A - sum_k L L^T) Dinv_jj^T),
+//        quadrant (r, 1) = partial update of A_{i_r, j+1}; x = 0 completes the
+//        diagonal tile A_{j+1, j+1} (look-ahead) with the fresh L_{j+1,j} L^T
+//   x >= nfp (eval): W columns jj1 = 2y, jj2 = 2y+1 (y = x - nfp, j even):
+//        quadrant (r, 0) = W_{j, jj_r}, quadrant (r, 1) = Vneg of W_{j+1, jj_r}
+// Nothing but the accumulators is live across the GEMM (the core takes all 128
+// VGPRs at 4 waves per SIMD; even loading A_ij into the accumulators before it
+// spills), and the epilogue
+// empties the accumulators into LDS first: the column-(j+1) quadrants go out
+// as partial updates, then both S tiles are staged (row-major, stride SLD) and
+// the two triangular products S_r Dinv_jj^T run together, each wave holding
+// its Dinv_jj operand fragments in registers.
+__host__ __device__ inline int nslot4_factor(int T, int j) { return (T - j) >> 1; }  // ceil((T-1-j)/2)
+
+// quadrant (qr, 1) of a gemm4 accumulator staged as X[n*XLD + m] (dst's storage order)
+__device__ __forceinline__ void stage4_q1(const Quad8& acc, int qr, double* X) {
+  const int w = threadIdx.x >> 6;
+  if ((w >> 2) == qr && (w & 1) == 1) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) X[(acc4_col(nb) - 64) * XLD + (acc4_row(mb, r) - 64 * qr)] = acc.c[mb][nb][r];
+  }
+}
+
+// Both triangular products out_r(m, n) = sum_q S_r(m, q) Dinv[n][q], S_r = A_r - acc
+// of quadrant (r, 0) (A_r column-major, null: S_r = -acc), r = 0, 1 (`two`):
+// stages S_r at lds + r * 64 * SLD (row-major; A_r added with coalesced reads),
+// wave w computes row block w & 3 of both tiles against column blocks {0, 3}
+// (w < 4) or {1, 2} (20 + 20 MFMAs); returns with the products in o[r][0..1].
+__device__ __forceinline__ void post_right4x2(const Quad8& acc, double* lds, const double* Dj, bool two,
+                                              const double* A0, const double* A1, d4 (&o)[2][2]) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int mb = w & 3, nA = (w >> 2) ? 1 : 0, nB = 3 - nA;
+  if ((w & 1) == 0) {
+    const int qr = w >> 2;
+    if (qr == 0 || two) {
+      double* S = lds + qr * NB * SLD;
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S[(acc4_row(m2, r) - 64 * qr) * SLD + acc4_col(nb)] = -acc.c[m2][nb][r];
+    }
+  }
+  // (the accumulators are dead from here on)
+  // B(k, n) = Dinv[n][k] at Dj[k*64 + n]: this wave's column blocks nA, nB, k-steps kk <= 4 nX + 3
+  double bA[8], bB[16];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) bA[kk] = kk <= 4 * nA + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * nA + fr) : 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) bB[kk] = kk <= 4 * nB + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * nB + fr) : 0.0;
+  if (A0) {  // S_r += A_r: element (m, q) at q*64 + m, read coalesced (8 per thread and tile)
+    double av[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      av[u] = gld(A0 + t + GEMM_THREADS * u);
+      bv[u] = two ? gld(A1 + t + GEMM_THREADS * u) : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = t + GEMM_THREADS * u, q = e >> 6, m = e & 63;
+      lds[m * SLD + q] += av[u];
+      if (two) lds[NB * SLD + m * SLD + q] += bv[u];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    o[r][0] = (d4){0.0, 0.0, 0.0, 0.0};
+    o[r][1] = o[r][0];
+    if (r == 1 && !two) break;
+    const double* S = lds + r * NB * SLD;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const double a = S[(16 * mb + fr) * SLD + 4 * kk + fk];
+      if (kk <= 4 * nA + 3) o[r][0] = MFMA64(a, bA[kk < 8 ? kk : 7], o[r][0]);
+      if (kk <= 4 * nB + 3) o[r][1] = MFMA64(a, bB[kk], o[r][1]);
+    }
+  }
+}
+
+// out tile r (o[r]) staged as X[n*XLD + m] (emit_copy / fwd_update / alpha_update layout)
+__device__ __forceinline__ void stage_post4(const d4 (&o)[2][2], int r, double* X) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, mb = w & 3, nA = (w >> 2) ? 1 : 0, nB = 3 - nA;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = 16 * mb + (lane >> 4) + 4 * q;
+    X[(16 * nA + fr) * XLD + m] = o[r][0][q];
+    X[(16 * nB + fr) * XLD + m] = o[r][1][q];
+  }
+}
+
+__global__ __launch_bounds__(GEMM_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list, int j, int gx, int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM4_LDS];
+  static_assert(2 * NB * SLD <= GEMM4_LDS && 2 * NB * XLD <= GEMM4_LDS, "panel4 staging must fit");
+  int ci, x;
+  if (!xcd_cell_slot(gx, ncell, ci, x)) return;
+  const OiCell& c = cells[list[ci]];
+  const int T = c.T;
+  if (j >= T || *c.status != OI_OK) return;
+  const int nfp = nslot4_factor(T, j);
+  const bool has_next = j + 1 < T;
+  const double* Dj = tileD(c, j);
+  const int rT = c.n - NB * (T - 1);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+  Quad8 acc;
+  quad8_zero(acc);
+  d4 o[2][2];
+  if (x < nfp) {
+    const int i1 = j + 1 + 2 * x, i2 = i1 + 1;
+    const bool two = i2 < T;
+    const int ti = wr >= 2 ? i2 : i1, tj = wc ? j + 1 : j;
+    unsigned skip = 0;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int m0 = 32 * (wr & 1) + 16 * mb, n0 = 16 * nb;
+        const bool off = ti >= T || (ti == T - 1 && m0 >= rT) || (tj == T - 1 && n0 >= rT) ||
+                         (x == 0 && wr < 2 && wc == 1 && m0 + 15 < n0);
+        if (off) skip |= 1u << (4 * mb + nb);
+      }
+    auto fpair = [=, &c](int p, const double*& a0, const double*& a1, const double*& b0, const double*& b1) {
+      a0 = tileL(c, i1, p);
+      a1 = two ? tileL(c, i2, p) : g_zero_tile;
+      b0 = tileL(c, j, p);
+      b1 = tileL(c, j + 1, p);
+    };
+    const bool masked = x == 0 || i2 >= T - 1 || j + 1 == T - 1;
+    if (masked)
+      gemm4_kmajor<true>(acc, lds, 4 * j, skip, fpair);
+    else
+      gemm4_kmajor<false>(acc, lds, 4 * j, 0u, fpair);
+    __syncthreads();  // the GEMM's last LDS reads are done
+    // column j+1: partial updates of A_{i_r, j+1} (x = 0: the diagonal tile, whose
+    // L_{j+1,j} L_{j+1,j}^T part follows once that tile is final)
+    stage4_q1(acc, 0, lds);
+    if (two) stage4_q1(acc, 1, lds + NB * XLD);
+    __syncthreads();
+    emit_copy(lds, tileL(c, i1, j + 1), EMIT_SUB);
+    if (two) emit_copy(lds + NB * XLD, tileL(c, i2, j + 1), EMIT_SUB);
+    __syncthreads();
+    post_right4x2(acc, lds, Dj, two, tileL(c, i1, j), two ? tileL(c, i2, j) : nullptr, o);
+    const double pre1 = fwd_preload(c, i1, j);
+    const double pre2 = two ? fwd_preload(c, i2, j) : 0.0;
+    __syncthreads();
+    stage_post4(o, 0, lds);  // L_{i1,j}
+    __syncthreads();
+    emit_copy(lds, tileL(c, i1, j), EMIT_STORE);
+    fwd_update<GEMM_THREADS>(c, lds, XLD, i1, pre1, lds + NB * XLD);
+    if (x == 0) {
+      // A_{j+1,j+1} -= L_{j+1,j} L_{j+1,j}^T: the fresh tile is staged as X[q*XLD + m]
+      // = L[m][q]; its 10 lower 16x16 blocks go to the 8 waves (blocks w, w + 8)
+      double* Y = lds + NB * XLD;
+      __syncthreads();  // fwd_update's scratch (= Y) is free
+      for (int e = t; e < OI_TILE; e += GEMM_THREADS) Y[(e >> 6) * XLD + (e & 63)] = 0.0;
+      __syncthreads();
+      const int fr = lane & 15, fk = lane >> 4;
+      for (int bidx = w; bidx < 10; bidx += 8) {
+        const int bm = bidx >= 6 ? 3 : bidx >= 3 ? 2 : bidx >= 1 ? 1 : 0, bn = bidx - bm * (bm + 1) / 2;
+        d4 s = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int kk = 0; kk < NB / 4; ++kk) {
+          const int q = 4 * kk + fk;
+          s = MFMA64(lds[q * XLD + 16 * bm + fr], lds[q * XLD + 16 * bn + fr], s);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Y[(16 * bn + fr) * XLD + 16 * bm + (lane >> 4) + 4 * r] = s[r];
+      }
+      __syncthreads();
+      emit_copy(Y, tileL(c, i1, i1), EMIT_SUB);
+    }
+    if (!two) return;
+    __syncthreads();
+    stage_post4(o, 1, lds);  // L_{i2,j}
+    __syncthreads();
+    emit_copy(lds, tileL(c, i2, j), EMIT_STORE);
+    fwd_update<GEMM_THREADS>(c, lds, XLD, i2, pre2, lds + NB * XLD);
+    return;
+  }
+  const int y = x - nfp;
+  if (c.mode != OI_MODE_EVAL || 2 * y >= j) return;
+  const int jj1 = 2 * y, jj2 = jj1 + 1;
+  const int tj = wc ? j + 1 : j;
+  unsigned skip = 0;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const int n0 = 16 * nb;
+      if ((wc == 1 && !has_next) || (tj == T - 1 && n0 >= rT)) skip |= 1u << (4 * mb + nb);
+    }
+  auto wpair = [=, &c](int p, const double*& a0, const double*& a1, const double*& b0, const double*& b1) {
+    const int k = jj1 + p;
+    a0 = tileW(c, k, jj1);
+    a1 = k >= jj2 ? tileW(c, k, jj2) : g_zero_tile;
+    b0 = tileL(c, j, k);
+    b1 = has_next ? tileL(c, j + 1, k) : g_zero_tile;
+  };
+  if (j >= T - 2)
+    gemm4_kmajor<true>(acc, lds, 4 * (j - jj1), skip, wpair);
+  else
+    gemm4_kmajor<false>(acc, lds, 4 * (j - jj1), 0u, wpair);
+  __syncthreads();
+  if (has_next) {  // Vneg of W_{j+1, jj_r}
+    stage4_q1(acc, 0, lds);
+    stage4_q1(acc, 1, lds + NB * XLD);
+    __syncthreads();
+    emit_copy(lds, tileW(c, j + 1, jj1), EMIT_NEG);
+    emit_copy(lds + NB * XLD, tileW(c, j + 1, jj2), EMIT_NEG);
+    __syncthreads();
+  }
+  post_right4x2(acc, lds, Dj, true, nullptr, nullptr, o);
+  const double apre1 = alpha_preload(c, jj1, j);
+  const double apre2 = alpha_preload(c, jj2, j);
+  __syncthreads();
+  stage_post4(o, 0, lds);  // W_{j,jj1}^T
+  __syncthreads();
+  emit_copy(lds, tileW(c, j, jj1), EMIT_STORE);
+  alpha_update<GEMM_THREADS>(c, lds, XLD, jj1, apre1, lds + NB * XLD);
+  __syncthreads();
+  stage_post4(o, 1, lds);  // W_{j,jj2}^T
+  __syncthreads();
+  emit_copy(lds, tileW(c, j, jj2), EMIT_STORE);
+  alpha_update<GEMM_THREADS>(c, lds, XLD, jj2, apre2, lds + NB * XLD);
 }
 
 // ------------------------------------------------------ k_lauum_grad
@@ -1776,6 +2026,15 @@ extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, in
   else
     hipLaunchKernelGGL(k_panel_even<true>, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells,
                        list, j, gx, ncell);
+  return ret();
+}
+
+extern "C" int oi_launch_panel4(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
+                                int with_trtri, void* stream) {
+  const int gx = nslot4_factor(maxT, j) + (with_trtri ? j / 2 : 0);
+  if (ncell <= 0 || gx <= 0) return 0;
+  hipLaunchKernelGGL(k_panel4, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j, gx,
+                     ncell);
   return ret();
 }
 

@@ -49,14 +49,17 @@ def expected_sites(sizes, grid_m=25e3, radius_m=300e3, t_days=9):
     return S * -np.expm1(-n / S)
 
 
-# E(n): SMLII evaluations per opt=True cell.  Refitted on the build's own day
-# run (bench.py --dump: info[:, 3] of the 9997 timed cells, round 3), linear in n
-EVALS_A, EVALS_B = 85.0, 0.045
+# E(n): SMLII evaluations per opt=True cell, least squares on the build's own
+# day run (bench.py --dump: info[:, 3] of the 9997 timed cells on MI355X, round
+# 3; tests/golden/day_cells_r03.npz): 90.3 per cell at n ~ 300..600 rising to
+# 102.7 at 2700..3000 (SURVEY §6's CPU fit, 85 + 0.045 (n - 300), was made on
+# 6 cells and overstates the growth 8x)
+EVALS_A, EVALS_B = 86.7, 0.0053
 
 
 def evals_model(sizes):
     n = np.asarray(sizes, dtype=np.float64)
-    return EVALS_A + EVALS_B * np.maximum(n - 300.0, 0.0)
+    return EVALS_A + EVALS_B * n
 
 
 def cell_costs(sizes, opt=True, sites=None):

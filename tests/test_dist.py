@@ -74,6 +74,29 @@ def test_partitions_cover_every_cell_once():
     assert max(loads) / min(loads) < 1.01
 
 
+def test_lpt_balances_realised_work_of_the_day():
+    """The 8-way (and 2-, 4-way) LPT split of the synthetic day, made on the
+    cost model (E(n) refitted, m = distinct sites; and m estimated from n for
+    config 5, where a rank has not drawn the observations), balances the work
+    the GPU actually did -- sum over a rank's cells of E_c (m_c^3 + 40 m_c^2)
+    with E_c the cell's measured SMLII evaluations (tests/golden/
+    day_cells_r03.npz, the timed cells of a bench.py run on MI355X) -- within
+    2 % of the mean rank (GPR:18-23, :256 scatter the cells)."""
+    from conftest import load_golden
+    d = load_golden('day_cells_r03.npz')
+    n, m, e = d['n'].astype(float), d['m'].astype(float), d['evals'].astype(float)
+    work = e * (m ** 3 + 40 * m ** 2)
+    # the refitted E(n) tracks the measured mean evaluations per n bucket within 3 %
+    for lo in range(300, 3000, 300):
+        s = (n >= lo) & (n < lo + 300)
+        assert abs(driver.evals_model(n[s]).mean() / e[s].mean() - 1) < 0.03, lo
+    for world in (2, 4, 8):
+        for sites in (m, driver.expected_sites(n)):
+            parts = driver.lpt_partition(driver.cell_costs(n, sites=sites), world)
+            loads = np.array([work[p].sum() for p in parts])
+            assert loads.max() / loads.mean() < 1.02, (world, loads / loads.mean())
+
+
 def _allgather_worker(rank, world, port, q):
     import torch.distributed as dist
     from optimalinterpolation_amd import day

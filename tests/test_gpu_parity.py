@@ -186,7 +186,8 @@ def test_panel_schemes_agree(scheme, monkeypatch):
         assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
 
 
-@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4'), ('OI_PFORM', '1')])
+@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4'), ('OI_PFORM', '1'), ('OI_PANEL4', '1'),
+                                        ('OI_PANEL4', '0')])
 def test_alternate_kernels_agree(knob, value, monkeypatch):
     """The A/B alternates kept in the library -- round 1's 32-blocked diagonal
     factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r), the
@@ -311,3 +312,31 @@ def test_duplicate_nonpd_band():
         if gpu_fail != ref_fail:
             (inband if tau / 5 <= r <= 5 * tau else disagree_outside).append((n, r, ref_fail, gpu_fail))
     assert not disagree_outside, (disagree_outside, inband)
+
+
+def test_panel4_equals_panel_even(monkeypatch):
+    """k_panel4 (two block rows per workgroup on the 128 x 128 core) does the
+    even-column panel's arithmetic in the same order as k_panel_even (same
+    MFMA chunk sequence, S = A - acc, the same triangular product) except the
+    look-ahead diagonal tile, (A - acc) - L L^T instead of A - (acc + L L^T):
+    objective, gradient and predictions agree to rounding (1e-12 relative),
+    poisoned workspaces (OI_POISON=1) included -- nothing is read before it
+    is written -- and each variant is bitwise reproducible."""
+    sizes = [1, 40, 63, 64, 65, 128, 129, 191, 192, 193, 257, 700, 1100, 2000]
+    cells = synthetic.make_cells(sizes, seed=23)
+    h = np.tile(np.array([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(1e-3), 0.]), (len(sizes), 1))
+    mX = np.full(len(cells.z), cells.mean)
+    hyp = np.tile(synthetic.FIXED_HYPERS, (len(sizes), 1))
+    res = {}
+    for p4 in ('0', '1'):
+        for poison in ('0', '1'):
+            monkeypatch.setenv('OI_PANEL4', p4)
+            monkeypatch.setenv('OI_POISON', poison)
+            ev = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, h)
+            pr = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+            res[(p4, poison)] = (ev[0], ev[1], pr[0][:, :3])
+    for p4 in ('0', '1'):
+        for a, b in zip(res[(p4, '1')], res[(p4, '0')]):
+            assert np.array_equal(a, b), p4
+    for a, b in zip(res[('1', '0')], res[('0', '0')]):
+        assert np.all(np.abs(a - b) <= 1e-12 * np.maximum(1.0, np.abs(b))), np.max(np.abs(a - b) / np.maximum(1, np.abs(b)))
