@@ -121,9 +121,9 @@ size_t cell_bytes(int64_t n, bool eval, bool ptiles) {
 }
 
 // ------------------------------------------------------------- profiling
-enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_EVEN, K_LAUUM, K_FINAL, K_COUNT };
+enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_EVEN, K_LAUUM, K_FINAL, K_EVEN4, K_COUNT };
 const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_chol_panel",
-                                    "k_panel_even", "k_lauum_grad", "k_finalize"};
+                                    "k_panel_even", "k_lauum_grad", "k_finalize", "k_panel4"};
 
 // Panel scheme, read per call from OI_PANEL:
 //   2 (default): even/odd block-column pairs share one stream (k_panel_even +
@@ -145,12 +145,13 @@ bool pform_panels() {
   const char* e = getenv("OI_PFORM");
   return e && atoi(e) == 1;
 }
-// Even-column panel core, read per call from OI_PANEL4: 1 => k_panel4 (two
-// block rows per workgroup on the 128 x 128 gemm4 core), 0 => k_panel_even
+// Even-column panel core, read per call from OI_PANEL4: 1 (default) => k_panel4
+// (two block rows per workgroup on the 128 x 128 gemm4 core; day 137.2 vs
+// 135.5 cells/s back to back on one box, profiles/r03/), 0 => k_panel_even
 // (64 x 128 gemm2 core).  Post-form only.
 bool panel4_enabled() {
   const char* e = getenv("OI_PANEL4");
-  return e && atoi(e) == 1;
+  return !(e && atoi(e) == 0);
 }
 // Executed MFMA flops per cell and launch (profile mode), mirroring the
 // kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
@@ -914,12 +915,13 @@ class Engine {
       const bool empty_panel = j == maxT - 1 && ne == 0;
       if (empty_panel) {
       } else if (even) {
-        mark(K_EVEN, false);
-        if (panel4_ && !pform_)
+        const int ke = panel4_ && !pform_ ? K_EVEN4 : K_EVEN;
+        mark(ke, false);
+        if (ke == K_EVEN4)
           rc |= oi_launch_panel4(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
         else
           rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
-        mark(K_EVEN, true);
+        mark(ke, true);
       } else {
         mark(K_TRSM, false);
         rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
@@ -933,7 +935,7 @@ class Engine {
           if (empty_panel)
             continue;
           else if (even && panel4_ && !pform_)
-            kfl_[K_EVEN] += acct::panel4(cd.T, cd.n, j, ev);
+            kfl_[K_EVEN4] += acct::panel4(cd.T, cd.n, j, ev);
           else if (even)
             kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev, !pform_);
           else

@@ -1,18 +1,30 @@
-"""T3 at config-3 sizes: the GPU's GPR3D(opt=True) fit of
-cells with n = 500 .. 3000 observations against the REFERENCE's own fits
+"""T3 at config-3 and config-5 sizes: the GPU's
+GPR3D(opt=True) fit of 27 cells with n = 500 .. 5000 observations (three in
+every 500-wide bucket) against the REFERENCE's own fits
 (tests/golden/fit_large.npz, made by tests/golden/make_fit_large.py running
 GPR_CS2S3.py:143-191 in the build container on the original observation
 order and on 4 permutations of it).
 
 scipy's CG stops on line-search failure and its stopping point moves with
-rounding noise, so per cell the GPU fit must either reproduce the
-reference's outputs to 1e-6 or reach an nlZ no worse than the worst of the
-reference's own runs 0-3 (its permutation envelope); run 4 is a held-out
-reference sample judged by the same rule, and the GPU may miss the envelope
-no more often than it does (+10 % of the cells).  The optimiser's work must
-match too: per n bucket the GPU's mean SMLII evaluations per cell are within
-10 % of the reference's mean over its 5 runs (or inside the range the
-reference's own runs span)."""
+rounding noise, so the GPU fit is judged as one more sample
+of the reference's own noise:
+
+* per cell: the GPU reproduces the reference's outputs to 1e-6, or reaches an
+  nlZ no worse than the worst of the reference's runs 0-3 (its permutation
+  envelope, + 1e-8 relative); run 4 is a held-out reference sample judged by
+  the same rule, and the GPU may miss the envelope no more often than it does
+  (+ one cell);
+* fleet: the median over cells of the fs relative error against
+  the reference's run 0 is <= 1e-8, and the fraction of cells beyond 1e-6 is
+  no larger than the fraction of the reference's own permuted runs 1-4 that
+  are beyond 1e-6 of its run 0 (+ one cell of slack for 27 samples);
+* work: per 500-wide n bucket the GPU's mean SMLII evaluations per cell are
+  within 10 % of the mean over the reference's 5 runs.
+
+The GPU's nlZ at its own fitted hypers comes from oi_nlml_grad_batch (T1-equal
+to the reference's SMLII to ~1e-13, tests/test_gpu_parity.py); the
+reference's nlZ values are the fixture's (computed by the reference's SMLII on
+the original order)."""
 import numpy as np
 import pytest
 
@@ -23,38 +35,78 @@ from optimalinterpolation_amd import _lib
 pytestmark = pytest.mark.gpu
 
 
-def nlz_at(hyp5, x, y, mean):
-    """The reference's objective (oracle, bit-identical to SMLII GPR:107-141) at
-    linear hypers, on the original observation order."""
-    f, _ = O.neg_log_ml(np.r_[np.log(hyp5), np.log(.1)], x, y, np.ones(len(y)) * mean)
-    return float(np.asarray(f).item()) if np.ndim(f) else float(f)
-
-
-def test_config3_size_fits_against_reference():
+def _fit():
     d = load_golden('fit_large.npz')
     x, y, offs, xs, mean = d['x'].reshape(-1, 3), d['y'], d['offs'], d['xs'], float(d['mean'])
-    out8, evals, nlz, sizes = d['out8'], d['evals'], d['nlz'], d['sizes']
-    ncell = len(sizes)
     out, status, info = _lib.gpr_batch(x, y, offs, xs, mean, x0=np.array(O.X0_PRODUCTION), opt=True,
                                        info=True)
-    assert np.all(status == 0) and np.isfinite(out).all()
+    h = np.column_stack([np.log(out[:, 3:8]), np.full(len(out), np.log(.1))])
+    nlz, _, st = _lib.nlml_grad_batch(x, y, np.full(len(y), mean), offs, h)
+    return d, out, status, info, nlz, st
+
+
+_CACHE = {}
+
+
+def fit():
+    if 'r' not in _CACHE:
+        _CACHE['r'] = _fit()
+    return _CACHE['r']
+
+
+def test_fixture_covers_config5_buckets():
+    d = load_golden('fit_large.npz')
+    sizes = d['sizes']
+    for lo in range(500, 5000, 500):
+        hi = lo + 500 if lo < 4500 else 5001
+        assert np.sum((sizes >= lo) & (sizes < hi)) >= 3, lo
+    assert sizes.max() == 5000 and d['out8'].shape[1] == 5
+
+
+def test_large_fits_per_cell_envelope():
+    d, out, status, info, nlz_gpu, st = fit()
+    out8, nlz = d['out8'], d['nlz']
+    ncell = len(d['sizes'])
+    assert np.all(status == 0) and np.isfinite(out).all() and np.all(st == 0)
     bad, bad_ref, report = [], [], []
     for c in range(ncell):
-        a, b = offs[c], offs[c + 1]
-        ref = out8[c, 0]
         f_env = max(nlz[c, :4])
         tol = 1e-8 * abs(nlz[c, 0]) + 1e-9
-        same = np.allclose(out[c], ref, rtol=1e-6, atol=0)
-        f_gpu = nlz_at(out[c, 3:8], x[a:b], y[a:b], mean)
-        report.append((int(sizes[c]), int(info[c, 3]), list(evals[c]), f_gpu - nlz[c, 0], f_env - nlz[c, 0]))
-        if not same and f_gpu > f_env + tol:
+        same = np.allclose(out[c], out8[c, 0], rtol=1e-6, atol=0)
+        report.append((int(d['sizes'][c]), int(info[c, 3]), list(d['evals'][c]), nlz_gpu[c] - nlz[c, 0],
+                       f_env - nlz[c, 0]))
+        if not same and nlz_gpu[c] > f_env + tol:
             bad.append(report[-1])
         if nlz[c, 4] > f_env + tol:
             bad_ref.append(c)
-    assert len(bad) <= len(bad_ref) + 0.1 * ncell, (bad, bad_ref, report)
-    for n in np.unique(sizes):
-        m = sizes == n
+    assert len(bad) <= len(bad_ref) + 1, (bad, bad_ref, report)
+
+
+def test_large_fits_fleet_rules():
+    d, out, status, info, nlz_gpu, st = fit()
+    out8, sizes = d['out8'], d['sizes']
+    ref_fs = out8[:, 0, 0]
+    rel = np.abs(out[:, 0] - ref_fs) / np.abs(ref_fs)
+    rel_ref = np.abs(out8[:, 1:, 0] - ref_fs[:, None]) / np.abs(ref_fs[:, None])   # permuted runs 1-4
+    frac_gpu = float(np.mean(rel > 1e-6))
+    frac_ref = float(np.mean(rel_ref > 1e-6))
+    print(f"fs rel-err vs reference run 0: median {np.median(rel):.2e}, > 1e-6 in {frac_gpu:.3f} of cells; "
+          f"reference's permuted runs: median {np.median(rel_ref):.2e}, > 1e-6 in {frac_ref:.3f}")
+    assert np.median(rel) <= 1e-8, np.sort(rel)
+    assert frac_gpu <= frac_ref + 1.0 / len(sizes), (frac_gpu, frac_ref, rel)
+
+
+def test_large_fits_evaluations_per_bucket():
+    d, out, status, info, nlz_gpu, st = fit()
+    sizes, evals = d['sizes'], d['evals']
+    lines = []
+    for lo in range(500, 5000, 500):
+        hi = lo + 500 if lo < 4500 else 5001
+        m = (sizes >= lo) & (sizes < hi)
         g = float(np.mean(info[m, 3]))
         r = float(np.mean(evals[m]))
-        lo, hi = float(evals[m].min()), float(evals[m].max())
-        assert abs(g / r - 1) <= 0.10 or lo <= g <= hi, (int(n), g, r, lo, hi, report)
+        lines.append((lo, g, r, g / r))
+    print("n bucket, GPU evals/cell, reference evals/cell, ratio:",
+          [(lo, round(g, 1), round(r, 1), round(q, 3)) for lo, g, r, q in lines])
+    for lo, g, r, q in lines:
+        assert abs(q - 1) <= 0.10, (lo, g, r, lines)
