@@ -299,7 +299,24 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline):
     # sample, added per evaluation (an additive term: it does not grow with n^3)
     ovh = [(f['fit_s'] - f['evals'] * t_eval(f['n']) - t_pred(f['n'])) / f['evals'] for f in fits]
     c_ovh = max(0.0, float(np.median(ovh)))
-    t_cells = rho * gpu_evals * (t_eval(n) + c_ovh) + t_pred(n)
+    # the CPU's evaluations per cell: the reference's OWN fits -- the 16 sample
+    # fits here and GPR_CS2S3.py:143-191 run on 27 cells of n = 500 .. 5000 x 5
+    # observation orders in the build container (tests/golden/fit_large.npz) --
+    # fitted a + b n; the GPU's per-cell counts x the small-n ratio as fallback
+    e_src = f"the GPU's per-cell evals x the CPU/GPU ratio {rho:.3f} at n <= 600"
+    e_cells = rho * gpu_evals
+    try:
+        fx = np.load(os.path.join(ROOT, 'tests', 'golden', 'fit_large.npz'))
+        en = np.concatenate([np.repeat(fx['sizes'], fx['evals'].shape[1]), [f['n'] for f in fits]]).astype(float)
+        ee = np.concatenate([fx['evals'].ravel(), [f['evals'] for f in fits]]).astype(float)
+        ce_n, *_ = np.linalg.lstsq(np.stack([np.ones_like(en), en], 1), ee, rcond=None)
+        e_cells = ce_n[0] + ce_n[1] * n
+        e_src = (f"the reference's own evaluations per cell, {ce_n[0]:.1f} + {ce_n[1]:.4f} n fitted to its "
+                 f"{fx['evals'].size} fits of n = {int(fx['sizes'].min())}..{int(fx['sizes'].max())} "
+                 f"(tests/golden/fit_large.npz) and the {len(fits)} sample fits")
+    except Exception:
+        pass
+    t_cells = e_cells * (t_eval(n) + c_ovh) + t_pred(n)
     value = len(n) / (float(np.sum(t_cells)) / workers)
     return {"value": value, "unit": "grid-cells/s", "cores": workers, "kind": "port",
             "sample": (f"oracle/gp_oracle.py (bit-exact restatement of GPR_CS2S3.py:78-191 + scipy CG) on "
@@ -307,10 +324,11 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline):
                        f"one predict at n={ns} x3 reps (median, fitted a+bn^2+cn^3) and {len(fits)} full "
                        f"GPR3D(opt=True) fits at n=300..600 (CPU {e_cpu:.1f} evals/cell vs GPU "
                        f"{e_gpu_small:.1f} on the day's n<=600 cells, ratio {rho:.3f}); extrapolated to the "
-                       f"{len(n)} timed cells with the GPU's per-cell evals x that ratio, plus the fits' "
+                       f"{len(n)} timed cells with {e_src}, plus the fits' "
                        f"measured per-evaluation optimiser overhead ({c_ovh * 1e3:.2f} ms) "
                        f"({time.time() - t0:.0f} s wall): extrapolated"),
             "e_cpu_small": round(e_cpu, 2), "e_gpu_small": round(e_gpu_small, 2),
+            "e_cpu_mean_timed_cells": round(float(np.mean(e_cells)), 2),
             "overhead_ms_per_eval": round(c_ovh * 1e3, 3),
             "probe_s": {str(k): [round(v[0], 5), round(v[1], 5)] for k, v in med.items()},
             "cpu_s_per_cell_mean": round(float(np.mean(t_cells)), 3)}
