@@ -73,6 +73,9 @@ def parse():
     p.add_argument('--budget-s', type=float, default=420.0,
                    help='wall-clock budget from process start; stop submitting slices beyond it')
     p.add_argument('--nys-cells', type=int, default=0, help='nystrom workload: cells per rank-step')
+    p.add_argument('--nys-oneshot', action='store_true',
+                   help='nystrom workload: one blocking oi_nystrom_fit_batch call per step (round 2) instead '
+                        'of a session fed one batch per step')
     p.add_argument('--svgp-cells', type=int, default=256, help='svgp workload: cells per rank-step')
     p.add_argument('--svgp-iters', type=int, default=10000, help='svgp workload: Adam steps per cell')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -394,6 +397,20 @@ def main_nystrom(args, torch, dist, world, rank, gpu, cdev):
         return _lib.nystrom_fit_batch(xd, yd, cells.offs, sel, soffs, x0, cells.xs, cells.mean,
                                       device=gpu, device_inputs=True, profile=profile)
 
+    def run_session(ks):  # one batch per step through a session: step k waits for step k - depth
+        outs, tickets = {}, {}
+        with _lib.NystromSession(device=gpu, device_inputs=True, profile=True) as sess:
+            for i, k in enumerate(ks):
+                cells, sel, soffs, xd, yd = steps[k]
+                tickets[k] = sess.submit(xd, yd, cells.offs, sel, soffs, x0, cells.xs, cells.mean)
+                if i >= args.depth:
+                    kk = ks[i - args.depth]
+                    outs[kk] = sess.wait(tickets[kk])
+            for k in ks:
+                if k not in outs:
+                    outs[k] = sess.wait(tickets[k])
+        return [outs[k] for k in ks]
+
     if not args.no_prime:  # library / rocBLAS / rocSOLVER initialisation, not a step
         pc = synthetic.make_cells([300], seed=4321)
         ps, po = nystrom._ragged_sel(pc.offs, 60)
@@ -405,7 +422,10 @@ def main_nystrom(args, torch, dist, world, rank, gpu, cdev):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    outs = [run(k, True) for k in range(args.warmup, args.warmup + args.steps)]
+    if args.nys_oneshot:
+        outs = [run(k, True) for k in range(args.warmup, args.warmup + args.steps)]
+    else:
+        outs = run_session(list(range(args.warmup, args.warmup + args.steps)))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -439,7 +459,9 @@ def main_nystrom(args, torch, dist, world, rank, gpu, cdev):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded cells of the SURVEY §8d generator)",
             "config": {"workload": f"Nystrom (GP_example.ipynb cell 5): {ncell} cells x n={NYS_N}, "
-                                   f"M={NYS_M} per rank per step, CG fit + predict",
+                                   f"M={NYS_M} per rank per step, CG fit + predict"
+                                   + (", one blocking call per step" if args.nys_oneshot else
+                                      f", one batch per step through a fit session (depth {args.depth})"),
                        "cells_per_step": ncell * world},
             "evals_per_cell": round(float(np.mean(evals)), 2), "roofline": roofline}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

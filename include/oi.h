@@ -191,6 +191,24 @@ int oi_nystrom_fit_batch(const double* xyt, const double* y, const int64_t* offs
                          const double* xs, double mean, double* out, int32_t* status,
                          int32_t* info, const oi_options* opts);
 
+/* Nystrom fits as a stream of batches (continuous batching across calls, as
+ * oi_session_* for the full GP): every submitted batch (oi_nystrom_fit_batch's
+ * arguments; host copies of offs, sel, soffs, x0, xs are taken, DEVICE inputs
+ * and all outputs must stay valid until the ticket completes) joins one queue;
+ * up to OI_NYS_CAP (32) cells per stream group fit at once and finished cells
+ * are replaced from the queue, so a batch's slowest cells overlap later
+ * batches.  Per-cell results equal oi_nystrom_fit_batch's bit for bit.
+ *   submit returns a ticket >= 0 (or a negative OI_E* code); wait runs rounds
+ *   until the ticket completes (ticket < 0: all submitted work). */
+typedef struct oi_nystrom_session oi_nystrom_session;
+oi_nystrom_session* oi_nystrom_session_create(const oi_options* opts);
+int64_t oi_nystrom_session_submit(oi_nystrom_session* s, const double* xyt, const double* y,
+                                  const int64_t* offs, int64_t ncell, const int64_t* sel,
+                                  const int64_t* soffs, const double* x0, const double* xs, double mean,
+                                  double* out, int32_t* status, int32_t* info);
+int oi_nystrom_session_wait(oi_nystrom_session* s, int64_t ticket);
+void oi_nystrom_session_destroy(oi_nystrom_session* s);
+
 /* ---- SVGP variant (dev/sparseGP_example.ipynb code cell 5: GPflow SVGP with a
  * Matern32 kernel, Gaussian likelihood, Constant mean, whitened q(u), trained
  * by TF2 Adam on minibatches, then predict_f) -- one workgroup per cell runs

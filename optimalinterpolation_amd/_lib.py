@@ -37,7 +37,8 @@ EXPORTS = ('oi_options_default', 'oi_gpr_batch', 'oi_nlml_grad_batch', 'oi_cg_cr
            'oi_ball_query', 'oi_gather_rows', 'oi_nystrom_batch',
            'oi_nystrom_fit_batch', 'oi_svgp_batch', 'oi_svgp_param_count', 'oi_session_create',
            'oi_session_submit', 'oi_session_set_stream', 'oi_session_wait', 'oi_session_done',
-           'oi_session_destroy')
+           'oi_session_destroy', 'oi_nystrom_session_create', 'oi_nystrom_session_submit',
+           'oi_nystrom_session_wait', 'oi_nystrom_session_destroy')
 
 
 class OiOptions(ctypes.Structure):
@@ -119,6 +120,17 @@ def load():
                                       c_double_p, c_double_p, c_double_p, c_int32_p,
                                       ctypes.POINTER(OiOptions)]
         lib.oi_svgp_batch.restype = ctypes.c_int
+        lib.oi_nystrom_session_create.argtypes = [ctypes.POINTER(OiOptions)]
+        lib.oi_nystrom_session_create.restype = ctypes.c_void_p
+        lib.oi_nystrom_session_submit.argtypes = [ctypes.c_void_p, c_double_p, c_double_p, c_int64_p,
+                                                  ctypes.c_int64, c_int64_p, c_int64_p, c_double_p,
+                                                  c_double_p, ctypes.c_double, c_double_p, c_int32_p,
+                                                  c_int32_p]
+        lib.oi_nystrom_session_submit.restype = ctypes.c_int64
+        lib.oi_nystrom_session_wait.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        lib.oi_nystrom_session_wait.restype = ctypes.c_int
+        lib.oi_nystrom_session_destroy.argtypes = [ctypes.c_void_p]
+        lib.oi_nystrom_session_destroy.restype = None
         lib.oi_session_create.argtypes = [ctypes.POINTER(OiOptions)]
         lib.oi_session_create.restype = ctypes.c_void_p
         lib.oi_session_submit.argtypes = [ctypes.c_void_p, c_double_p, c_double_p, c_int64_p,
@@ -451,6 +463,81 @@ def nystrom_fit_batch(xyt, y, offs, sel, soffs, x0, xs, mean, **opt_kw):
                                   _ptr(info, ctypes.c_int32), ctypes.byref(o))
     _check(rc)
     return out, status, info
+
+
+class NystromSession:
+    """oi_nystrom_session_*: Nystrom fits (oi_nystrom_fit_batch) as a stream of
+    batches with continuous batching across calls.  ``submit`` takes
+    nystrom_fit_batch's arguments and returns a ticket; ``wait(ticket)``
+    returns that batch's (out, status, info) once its last cell is fitted and
+    predicted.  Device inputs (``device_inputs=True``) must stay alive until
+    their ticket completes (the session keeps a reference)."""
+
+    def __init__(self, device=0, device_inputs=False, **opt_kw):
+        self._lib = load()
+        self.device = int(device)
+        self.device_inputs = bool(device_inputs)
+        self._opts = options(device=device, device_inputs=device_inputs, **opt_kw)
+        self._h = self._lib.oi_nystrom_session_create(ctypes.byref(self._opts))
+        if not self._h:
+            raise OiError(f"oi_nystrom_session_create: {self._lib.oi_last_error().decode(errors='replace')}")
+        self._live = {}
+
+    def submit(self, xyt, y, offs, sel, soffs, x0, xs, mean):
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        sel = np.ascontiguousarray(sel, dtype=np.int64)
+        soffs = np.ascontiguousarray(soffs, dtype=np.int64)
+        ncell = len(offs) - 1
+        x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(5)
+        xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(ncell, 3)
+        if self.device_inputs:
+            _check_dev(xyt, self.device, n=3 * int(offs[-1]), what='xyt')
+            _check_dev(y, self.device, n=int(offs[-1]), what='y')
+            px, py = _dptr(xyt), _dptr(y)
+            _sync_producers(self.device)
+        else:
+            xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+            y = np.ascontiguousarray(y, dtype=np.float64)
+            if offs[-1] != len(y) or xyt.shape[0] != len(y):
+                raise ValueError("inconsistent ragged batch")
+            px, py = _ptr(xyt, ctypes.c_double), _ptr(y, ctypes.c_double)
+        if len(soffs) != ncell + 1 or soffs[-1] != len(sel):
+            raise ValueError("inconsistent inducing rows")
+        out = np.empty((ncell, 8))
+        status = np.zeros(ncell, dtype=np.int32)
+        info = np.zeros((ncell, 4), dtype=np.int32)
+        t = self._lib.oi_nystrom_session_submit(self._h, px, py, _ptr(offs, ctypes.c_int64), ncell,
+                                                _ptr(sel, ctypes.c_int64), _ptr(soffs, ctypes.c_int64),
+                                                _ptr(x0, ctypes.c_double), _ptr(xs, ctypes.c_double),
+                                                float(mean), _ptr(out, ctypes.c_double),
+                                                _ptr(status, ctypes.c_int32), _ptr(info, ctypes.c_int32))
+        if t < 0:
+            _check(int(t))
+        self._live[int(t)] = (out, status, info, xyt, y)
+        return int(t)
+
+    def wait(self, ticket):
+        ticket = int(ticket)
+        if ticket not in self._live:
+            raise KeyError(f"unknown or already collected session ticket {ticket}")
+        _check(self._lib.oi_nystrom_session_wait(self._h, ticket))
+        out, status, info, _, _ = self._live.pop(ticket)
+        return out, status, info
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._lib.oi_nystrom_session_destroy(self._h)
+            self._h = None
+            self._live.clear()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        self.close()
 
 
 def svgp_batch(xyt, y, offs, Z0, init, xs, batch=100, iterations=10000, log_every=10, seed=0,

@@ -41,6 +41,7 @@
 #include <cstdlib>
 #include <memory>
 #include <cstdint>
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -467,6 +468,16 @@ int setup(const oi_options* opts, oi_options& o) {
   return 0;
 }
 
+// One cell's inputs on the device: the row of the cell table a Runner reads.
+struct CellSrc {
+  const double* x;     // n x 3
+  const double* y;     // n (outputs minus the prior mean, as NB1 passes them)
+  const int64_t* sel;  // M inducing rows, 0-based within the cell
+  const double* xs;    // 3 (prediction target) or null
+  int64_t n, M;
+};
+
+struct Buf;
 // Outcome of one cell at one hyper point (host side).
 struct CellOut {
   double nlz, grad[5], fs, sd, sprior;
@@ -488,6 +499,37 @@ struct Buf {
   template <class T>
   T* as() const {
     return static_cast<T*>(p);
+  }
+};
+
+// Device copy of one validated batch (inputs when they came from the host,
+// inducing rows, targets) and its rows of the cell table.
+struct BatchDev {
+  Buf hx, hy, dsel, dxs;
+  std::vector<CellSrc> rows;
+  BatchDev(const Batch& b, const double* xs, bool device_inputs) {
+    const int64_t N = b.offs[b.ncell], S = b.soffs[b.ncell];
+    const double* dx = b.xyt;
+    const double* dy = b.y;
+    if (!device_inputs) {
+      hx.alloc(N * 3 * 8);
+      hy.alloc(N * 8);
+      HC(hipMemcpy(hx.p, b.xyt, N * 3 * 8, hipMemcpyHostToDevice));
+      HC(hipMemcpy(hy.p, b.y, N * 8, hipMemcpyHostToDevice));
+      dx = hx.as<double>();
+      dy = hy.as<double>();
+    }
+    dsel.alloc(S * 8);
+    HC(hipMemcpy(dsel.p, b.sel, S * 8, hipMemcpyHostToDevice));
+    if (xs) {
+      dxs.alloc(b.ncell * 3 * 8);
+      HC(hipMemcpy(dxs.p, xs, b.ncell * 3 * 8, hipMemcpyHostToDevice));
+    }
+    rows.resize(b.ncell);
+    for (int64_t c = 0; c < b.ncell; ++c)
+      rows[c] = CellSrc{dx + b.offs[c] * 3, dy + b.offs[c], dsel.as<int64_t>() + b.soffs[c],
+                        xs ? dxs.as<double>() + c * 3 : nullptr, b.offs[c + 1] - b.offs[c],
+                        b.soffs[c + 1] - b.soffs[c]};
   }
 };
 
@@ -552,68 +594,54 @@ struct Lane {
 // K_mm -> u, s, st, C, B -> L) lives in chunk-sized slot arrays.
 class Runner {
  public:
-  // own_stream: work on a private stream (several Runners then overlap);
-  // otherwise on the caller's opts.stream
-  Runner(const Batch& b, const oi_options& o, bool want_obj, bool want_pred, const double* xs,
-         bool own_stream = false)
-      : b_(b), st_((hipStream_t)o.stream), alloc_obj_(want_obj), alloc_pred_(want_pred) {
+  // Reads cells from *tab (rows indexed by cell id; the table may grow between
+  // calls); every cell has n <= nmax, M <= mmax; at most `cap` cells per
+  // evaluation.  own_stream: work on a private stream (several Runners then
+  // overlap); otherwise on the caller's opts.stream
+  Runner(const std::vector<CellSrc>* tab, int64_t nmax, int64_t mmax, int64_t cap, const oi_options& o,
+         bool want_obj, bool want_pred, bool own_stream = false)
+      : tab_(tab), nmax_(nmax), cap_(cap), st_((hipStream_t)o.stream), alloc_obj_(want_obj),
+        alloc_pred_(want_pred) {
     if (own_stream) {
       HC(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
       own_ = true;
     }
-    const int64_t N = b.offs[b.ncell], S = b.soffs[b.ncell];
-    dx_ = b.xyt;
-    dy_ = b.y;
-    if (!o.device_inputs) {
-      hx_.alloc(N * 3 * 8);
-      hy_.alloc(N * 8);
-      HC(hipMemcpyAsync(hx_.p, b.xyt, N * 3 * 8, hipMemcpyHostToDevice, st_));
-      HC(hipMemcpyAsync(hy_.p, b.y, N * 8, hipMemcpyHostToDevice, st_));
-      dx_ = hx_.as<double>();
-      dy_ = hy_.as<double>();
-    }
-    dsel_.alloc(S * 8);
-    HC(hipMemcpyAsync(dsel_.p, b.sel, S * 8, hipMemcpyHostToDevice, st_));
-    if (want_pred) {
-      dxs_.alloc(b.ncell * 3 * 8);
-      HC(hipMemcpyAsync(dxs_.p, xs, b.ncell * 3 * 8, hipMemcpyHostToDevice, st_));
-    }
-    res_.alloc(b.ncell * NRES * 8);
-    info_.alloc(b.ncell * NINFO * sizeof(rocblas_int));
-    HC(hipHostMalloc((void**)&hr_, b.ncell * NRES * 8, hipHostMallocDefault));
-    HC(hipHostMalloc((void**)&hi_, b.ncell * NINFO * sizeof(rocblas_int), hipHostMallocDefault));
+    res_.alloc(cap * NRES * 8);
+    info_.alloc(cap * NINFO * sizeof(rocblas_int));
+    HC(hipHostMalloc((void**)&hr_, cap * NRES * 8, hipHostMallocDefault));
+    HC(hipHostMalloc((void**)&hi_, cap * NINFO * sizeof(rocblas_int), hipHostMallocDefault));
     BC(rocblas_set_stream(H_.h, st_));
     sg_.on = o.profile != 0;
     sg_.st = st_;
     int nl = 1;
     if (const char* e = getenv("OI_NYS_LANES")) nl = atoi(e);
     nl = nl < 1 ? 1 : nl;
-    nl = nl > b.ncell ? (int)b.ncell : nl;
+    nl = nl > cap ? (int)cap : nl;
     for (int l = 0; l < nl; ++l)
-      lanes_.emplace_back(new Lane(b.nmax, b.mmax, want_obj, want_pred, o.profile != 0));
+      lanes_.emplace_back(new Lane(nmax, mmax, want_obj, want_pred, o.profile != 0));
     // padding quantum for the batched factorisations (OI_NYS_PAD, default 32;
     // 0 = batch only cells of equal M): K_mm and B of a cell are factored as
     // diag(A, d I) of size Mp = M rounded up, so cells of different M share
     // one strided-batched call
     if (const char* e = getenv("OI_NYS_PAD")) padq_ = std::max(0, atoi(e));
-    mpmax_ = Mp(b.mmax);
+    mpmax_ = Mp(mmax);
     // slot arrays: sc, sq (n x 3), Kmm (Mp^2), s, st, E (Mp), C (n x M), B (Mp^2);
     // chunk <= 64 cells and <= 1/4 of the free HBM
-    const int64_t nmax = b.nmax, mmax = mpmax_;
-    const size_t per = (size_t)(6 * nmax + 2 * mmax * mmax + 3 * mmax + nmax * mmax) * 8;
+    const int64_t mmaxp = mpmax_;
+    const size_t per = (size_t)(6 * nmax + 2 * mmaxp * mmaxp + 3 * mmaxp + nmax * mmaxp) * 8;
     size_t fr = 0, tot = 0;
     HC(hipMemGetInfo(&fr, &tot));
-    int64_t ch = std::min<int64_t>(64, b.ncell);
+    int64_t ch = std::min<int64_t>(64, cap);
     ch = std::min<int64_t>(ch, std::max<int64_t>(1, (int64_t)(fr / 4 / per)));
     chunk_ = ch;
     sc_.alloc(ch * nmax * 3 * 8);
     sq_.alloc(ch * nmax * 3 * 8);
-    Kmm_.alloc(ch * mmax * mmax * 8);
-    eval_.alloc(ch * mmax * 8);
-    stl_.alloc(ch * mmax * 8);
-    E_.alloc(ch * mmax * 8);
-    C_.alloc(ch * nmax * mmax * 8);
-    B_.alloc(ch * mmax * mmax * 8);
+    Kmm_.alloc(ch * mmaxp * mmaxp * 8);
+    eval_.alloc(ch * mmaxp * 8);
+    stl_.alloc(ch * mmaxp * 8);
+    E_.alloc(ch * mmaxp * 8);
+    C_.alloc(ch * nmax * mmaxp * 8);
+    B_.alloc(ch * mmaxp * mmaxp * 8);
     info_tmp_.alloc(2 * ch * sizeof(rocblas_int));
     HC(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   }
@@ -639,6 +667,7 @@ class Runner {
     const int64_t nc = (int64_t)cells.size();
     ncq_ = nc;
     if (!nc) return;
+    if (nc > cap_) throw HipErr{"Runner: more cells than its capacity"};
     if ((want_obj && !alloc_obj_) || (want_pred && !alloc_pred_))
       throw HipErr{"Runner: stage not allocated"};
     obj_ = want_obj;
@@ -681,7 +710,7 @@ class Runner {
     const double inf = INFINITY, nan = NAN;
     for (int64_t p = 0; p < nc; ++p) {
       const int64_t k = order_[p], c = cells[k];
-      const int64_t n = b_.offs[c + 1] - b_.offs[c], M = Mof(c);
+      const int64_t n = (*tab_)[c].n, M = Mof(c);
       const double sf2 = hyp[k * 5 + 3], sn2 = hyp[k * 5 + 4];
       const double* rr = hr_ + p * NRES;
       const rocblas_int* ii = hi_ + p * NINFO;
@@ -713,7 +742,7 @@ class Runner {
   }
 
  private:
-  int64_t Mof(int64_t c) const { return b_.soffs[c + 1] - b_.soffs[c]; }
+  int64_t Mof(int64_t c) const { return (*tab_)[c].M; }
   int64_t Mp(int64_t M) const { return padq_ > 0 ? (M + padq_ - 1) / padq_ * padq_ : M; }
 
   // per-cell phase `ph` for positions [p0, p1) dealt over the lanes, fenced
@@ -791,7 +820,7 @@ class Runner {
     CellRefs R;
     R.k = order_[p];
     R.c = (*cells_)[R.k];
-    R.n = b_.offs[R.c + 1] - b_.offs[R.c];
+    R.n = (*tab_)[R.c].n;
     R.M = Mof(R.c);
     R.Mp = Mp(R.M);
     R.in = (int)R.n;
@@ -799,11 +828,11 @@ class Runner {
     R.iMp = (int)R.Mp;
     R.dn = (double)R.n;
     R.dM = (double)R.M;
-    R.x = dx_ + b_.offs[R.c] * 3;
-    R.r = dy_ + b_.offs[R.c];
-    R.sl = dsel_.as<int64_t>() + b_.soffs[R.c];
+    R.x = (*tab_)[R.c].x;
+    R.r = (*tab_)[R.c].y;
+    R.sl = (*tab_)[R.c].sel;
     R.hp = hyp_ + R.k * 5;
-    const int64_t nmax = b_.nmax, mmax = mpmax_;
+    const int64_t nmax = nmax_, mmax = mpmax_;
     R.sc = sc_.as<double>() + slot * nmax * 3;
     R.sq = sq_.as<double>() + slot * nmax * 3;
     R.Kmm = Kmm_.as<double>() + slot * mmax * mmax;
@@ -946,7 +975,7 @@ class Runner {
       sg.begin(S_PRED, 2.0 * dn * dM, 8.0 * dn * dM);
       double* ks = L.ks.as<double>();
       double* kv = L.kv.as<double>();
-      hipLaunchKernelGGL(k_nys_scale, dim3(1), dim3(64), 0, st, dxs_.as<double>() + R.c * 3,
+      hipLaunchKernelGGL(k_nys_scale, dim3(1), dim3(64), 0, st, (*tab_)[R.c].xs,
                          (int64_t)1, R.hp[0], R.hp[1], R.hp[2], L.xsc.as<double>(), nullptr);
       KCHK();
       hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), 1), dim3(256), 0, st, R.sc, nullptr,
@@ -964,12 +993,11 @@ class Runner {
     }
   }
 
-  const Batch& b_;
+  const std::vector<CellSrc>* tab_;
+  int64_t nmax_ = 0, cap_ = 0;
   hipStream_t st_;
   bool obj_ = false, pred_ = false, alloc_obj_, alloc_pred_;
-  const double* dx_;
-  const double* dy_;
-  Buf hx_, hy_, dsel_, dxs_, res_, info_;
+  Buf res_, info_;
   Buf sc_, sq_, Kmm_, eval_, stl_, E_, C_, B_, info_tmp_;
   int64_t chunk_ = 1;
   int padq_ = 32;
@@ -1021,7 +1049,8 @@ extern "C" int oi_nystrom_batch(const double* xyt, const double* y, const int64_
   oi_options o;
   if (int rc = setup(opts, o)) return rc;
   return guarded([&] {
-    Runner R(b, o, want_obj, want_pred, xs);
+    BatchDev bd(b, want_pred ? xs : nullptr, o.device_inputs != 0);
+    Runner R(&bd.rows, b.nmax, b.mmax, ncell, o, want_obj, want_pred);
     std::vector<int64_t> cells(ncell);
     for (int64_t c = 0; c < ncell; ++c) cells[c] = c;
     std::vector<CellOut> out(ncell);
@@ -1087,8 +1116,10 @@ extern "C" int oi_nystrom_fit_batch(const double* xyt, const double* y, const in
     G = std::max(1, std::min<int>(G, (int)ncell));
     std::vector<std::vector<int64_t>> gcells(G);
     for (int64_t c = 0; c < ncell; ++c) gcells[c % G].push_back(c);
+    BatchDev bd(b, xs, o.device_inputs != 0);
     std::vector<std::unique_ptr<Runner>> RG;
-    for (int g = 0; g < G; ++g) RG.emplace_back(new Runner(b, o, true, false, xs, G > 1));
+    for (int g = 0; g < G; ++g)
+      RG.emplace_back(new Runner(&bd.rows, b.nmax, b.mmax, (int64_t)gcells[g].size(), o, true, false, G > 1));
     std::vector<std::vector<int64_t>> qcells(G);
     std::vector<CellOut> res(ncell);
     auto queue = [&](int g) {
@@ -1121,7 +1152,7 @@ extern "C" int oi_nystrom_fit_batch(const double* xyt, const double* y, const in
       }
     }
     RG.clear();
-    Runner R(b, o, false, true, xs);
+    Runner R(&bd.rows, b.nmax, b.mmax, ncell, o, false, true);
     std::vector<int64_t> cells;
     std::vector<double> hyp;
     // NB1 code cell 5: GPR(approx=True) at the fitted hypers
@@ -1152,4 +1183,256 @@ extern "C" int oi_nystrom_fit_batch(const double* xyt, const double* y, const in
     }
     return 0;
   });
+}
+
+// ---- Nystrom fit session: continuous batching across calls (NB1 code cell 5
+// as a stream of batches).  Every submitted batch joins one queue of cells;
+// each of the G groups (own stream, Runner) keeps up to CAP cells fitting and
+// refills from the queue as cells finish, so a call's slowest cells overlap
+// the next calls' cells instead of idling the GPU (the one-shot fit waits for
+// its slowest cell).  A ticket completes when its last cell is fitted; its
+// predictions (GPR(approx=True) at the fitted hypers) run then.  Per-cell
+// arithmetic never depends on the other resident cells, so results equal
+// oi_nystrom_fit_batch's bit for bit.
+namespace {
+struct NysTicket {
+  std::unique_ptr<BatchDev> dev;
+  int64_t first = 0, count = 0, unfitted = 0;
+  double mean = 0.0;
+  double* out = nullptr;
+  int32_t* status = nullptr;
+  int32_t* info = nullptr;
+  bool done = false;
+};
+}  // namespace
+
+struct oi_nystrom_session {
+  oi_options o;
+  int G = 2;
+  int64_t cap = 32;  // resident fitting cells per group
+  int32_t maxiter = 1000;
+  double gtol = 1e-5;
+  std::vector<CellSrc> tab;          // every submitted cell, by global id
+  std::vector<int64_t> owner;        // cell -> ticket
+  std::vector<oi_cg*> cg;            // per cell (null before admission / after release)
+  std::vector<double> req;           // per cell: the requested point (6)
+  std::vector<double> x0;            // per cell: the batch's x0 (5)
+  std::deque<int64_t> queue;         // submitted, not admitted
+  std::vector<std::unique_ptr<NysTicket>> tickets;
+  int64_t nmax = 0, mmax = 0;        // the Runners' sizes
+  struct Grp {
+    std::unique_ptr<Runner> R;
+    std::vector<int64_t> active, inflight;
+  };
+  std::vector<Grp> grp;
+  std::unique_ptr<Runner> pred;      // predictions of completed tickets
+
+  ~oi_nystrom_session() {
+    for (auto* p : cg)
+      if (p) oi_cg_destroy(p);
+  }
+
+  void build_runners(int64_t nm, int64_t mm) {
+    nmax = std::max(nmax, nm);
+    mmax = std::max(mmax, mm);
+    grp.resize(G);
+    for (auto& g : grp) g.R.reset(new Runner(&tab, nmax, mmax, cap, o, true, false, G > 1));
+    pred.reset(new Runner(&tab, nmax, mmax, cap, o, false, true, true));
+  }
+
+  void feed(Grp& g) {  // collect a group's round, advance its cells' CG
+    if (g.inflight.empty()) return;
+    std::vector<CellOut> res(g.inflight.size());
+    g.R->collect(res.data());
+    for (size_t k = 0; k < g.inflight.size(); ++k) {
+      const int64_t c = g.inflight[k];
+      const double g6[6] = {res[k].grad[0], res[k].grad[1], res[k].grad[2], res[k].grad[3], res[k].grad[4], 0.0};
+      if (oi_cg_feed(cg[c], res[k].nlz, g6) != 0) throw HipErr{"oi_cg_feed failed"};
+      const int rc = oi_cg_step(cg[c], req.data() + c * 6);
+      if (rc < 0) throw HipErr{"oi_cg_step failed"};
+      if (rc == 0) finished(c);
+    }
+    g.inflight.clear();
+    std::vector<int64_t> keep;
+    for (int64_t c : g.active)
+      if (cg[c] && !fitted_[c]) keep.push_back(c);
+    g.active.swap(keep);
+  }
+
+  std::vector<char> fitted_;
+
+  void finished(int64_t c) {
+    fitted_[c] = 1;
+    NysTicket& t = *tickets[owner[c]];
+    if (--t.unfitted == 0) complete(t);
+  }
+
+  void complete(NysTicket& t) {
+    // GPR(approx=True) at the fitted hypers, in chunks of the Runner capacity
+    Runner& R = *pred;
+    std::vector<CellOut> res(cap);
+    for (int64_t a = 0; a < t.count; a += cap) {
+      const int64_t b = std::min(t.count, a + cap);
+      std::vector<int64_t> cells;
+      std::vector<double> hyp;
+      for (int64_t k = a; k < b; ++k) {
+        const int64_t c = t.first + k;
+        double xf[6], fun;
+        int32_t nit, cst;
+        int64_t nfev, njev, nobj;
+        oi_cg_result(cg[c], xf, &fun, &nit, &cst, &nfev, &njev, &nobj);
+        if (t.info) {
+          t.info[k * 4 + 0] = nit;
+          t.info[k * 4 + 1] = cst;
+          t.info[k * 4 + 2] = (int32_t)nfev;
+          t.info[k * 4 + 3] = (int32_t)nobj;
+        }
+        cells.push_back(c);
+        for (int q = 0; q < 5; ++q) hyp.push_back(std::exp(xf[q]));
+      }
+      R.run(cells, hyp.data(), t.mean, res.data(), false, true);
+      for (int64_t k = a; k < b; ++k) {
+        const CellOut& r = res[k - a];
+        t.status[k] = r.status;
+        t.out[k * 8 + 0] = r.fs;
+        t.out[k * 8 + 1] = r.sd;
+        t.out[k * 8 + 2] = r.sprior;
+        for (int q = 0; q < 5; ++q) t.out[k * 8 + 3 + q] = hyp[(k - a) * 5 + q];
+      }
+    }
+    for (int64_t k = 0; k < t.count; ++k) {
+      oi_cg_destroy(cg[t.first + k]);
+      cg[t.first + k] = nullptr;
+    }
+    t.done = true;
+    t.dev.reset();  // device inputs of the batch are no longer read
+  }
+
+  void admit(Grp& g) {
+    while ((int64_t)g.active.size() < cap && !queue.empty()) {
+      const int64_t c = queue.front();
+      queue.pop_front();
+      double x6[6];
+      for (int q = 0; q < 5; ++q) x6[q] = x0[c * 5 + q];
+      x6[5] = 0.0;
+      cg[c] = oi_cg_create(x6, gtol, maxiter);
+      if (!cg[c]) throw std::bad_alloc();
+      const int rc = oi_cg_step(cg[c], req.data() + c * 6);
+      if (rc < 0) throw HipErr{"oi_cg_step failed"};
+      if (rc == 0) {
+        finished(c);
+        continue;
+      }
+      g.active.push_back(c);
+    }
+  }
+
+  void launch(Grp& g) {  // one evaluation round of the group's live cells
+    g.inflight.clear();
+    std::vector<double> hyp;
+    for (int64_t c : g.active) {
+      g.inflight.push_back(c);
+      for (int q = 0; q < 5; ++q) hyp.push_back(std::exp(req[c * 6 + q]));  // NB1 SMLII
+    }
+    if (!g.inflight.empty()) g.R->enqueue(g.inflight, hyp.data(), tickets[owner[g.inflight[0]]]->mean, true, false);
+  }
+
+  // rounds until ticket t (all work when t < 0) is complete
+  void wait(int64_t t) {
+    while (true) {
+      if (t >= 0 && tickets[t]->done) return;
+      bool any = false;
+      for (auto& g : grp) {
+        feed(g);
+        admit(g);
+        launch(g);
+        any = any || !g.inflight.empty();
+      }
+      if (!any) {
+        if (t >= 0 && !tickets[t]->done) throw HipErr{"nystrom session: ticket cannot complete"};
+        return;
+      }
+    }
+  }
+
+  // every group idle (their rounds collected and fed), e.g. before the Runners are rebuilt
+  void drain() {
+    for (auto& g : grp) feed(g);
+  }
+};
+
+extern "C" oi_nystrom_session* oi_nystrom_session_create(const oi_options* opts) {
+  oi_options o;
+  if (setup(opts, o)) return nullptr;
+  auto* s = new oi_nystrom_session();
+  s->o = o;
+  s->maxiter = o.maxiter < 0 ? 1000 : o.maxiter;  // scipy: len(x0) * 200 for NB1's 5 hypers
+  s->gtol = o.gtol;
+  if (const char* e = getenv("OI_NYS_GROUPS")) s->G = std::max(1, atoi(e));
+  if (const char* e = getenv("OI_NYS_CAP")) s->cap = std::max(1, atoi(e));
+  return s;
+}
+
+extern "C" int64_t oi_nystrom_session_submit(oi_nystrom_session* s, const double* xyt, const double* y,
+                                             const int64_t* offs, int64_t ncell, const int64_t* sel,
+                                             const int64_t* soffs, const double* x0, const double* xs,
+                                             double mean, double* out, int32_t* status, int32_t* info) {
+  if (!s) return oi_set_last_error(OI_E_ARG, "null session");
+  Batch b{xyt, y, offs, ncell, sel, soffs};
+  if (int rc = check_batch(b)) return rc;
+  if (ncell > 0 && (!x0 || !xs || !out || !status)) return oi_set_last_error(OI_E_ARG, "null pointer");
+  int64_t ticket = -1;
+  const int rc = guarded([&] {
+    HC(hipSetDevice(s->o.device));
+    auto t = std::make_unique<NysTicket>();
+    t->first = (int64_t)s->tab.size();
+    t->count = ncell;
+    t->unfitted = ncell;
+    t->mean = mean;
+    t->out = out;
+    t->status = status;
+    t->info = info;
+    ticket = (int64_t)s->tickets.size();
+    if (ncell > 0) {
+      t->dev.reset(new BatchDev(b, xs, s->o.device_inputs != 0));
+      if (s->grp.empty() || b.nmax > s->nmax || b.mmax > s->mmax) {
+        s->drain();  // no round in flight over the old Runners' workspaces
+        s->build_runners(b.nmax, b.mmax);
+      }
+      for (int64_t c = 0; c < ncell; ++c) {
+        s->tab.push_back(t->dev->rows[c]);
+        s->owner.push_back(ticket);
+        s->cg.push_back(nullptr);
+        s->fitted_.push_back(0);
+        for (int q = 0; q < 6; ++q) s->req.push_back(0.0);
+        for (int q = 0; q < 5; ++q) s->x0.push_back(x0[q]);
+        s->queue.push_back(t->first + c);
+      }
+    } else {
+      t->done = true;
+    }
+    s->tickets.push_back(std::move(t));
+    return 0;
+  });
+  return rc ? rc : ticket;
+}
+
+extern "C" int oi_nystrom_session_wait(oi_nystrom_session* s, int64_t ticket) {
+  if (!s) return oi_set_last_error(OI_E_ARG, "null session");
+  if (ticket >= (int64_t)s->tickets.size()) return oi_set_last_error(OI_E_ARG, "unknown ticket");
+  return guarded([&] {
+    HC(hipSetDevice(s->o.device));
+    s->wait(ticket);
+    return 0;
+  });
+}
+
+extern "C" void oi_nystrom_session_destroy(oi_nystrom_session* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->o.device);
+  try {
+    s->drain();
+  } catch (...) {
+  }
+  delete s;
 }

@@ -107,6 +107,8 @@ def main():
     ap.add_argument('--jobs', type=int, default=8)
     ap.add_argument('--out', default=os.path.join(HERE, 'fit_large.npz'))
     ap.add_argument('--sizes', default='', help='comma list overriding SIZES (dry runs)')
+    ap.add_argument('--reverse', action='store_true',
+                    help='smallest cells first (a second generator sharing the cache works from the other end)')
     ap.add_argument('--merge', nargs='?', const='', default=None,
                     help='reuse the cells of an existing fixture (default: --out) whose sizes match')
     args = ap.parse_args()
@@ -128,7 +130,7 @@ def main():
                 res[(k, r)] = (old['out8'][k, r], int(old['evals'][k, r]), ox[a:b], oy[a:b], sec)
         print(f"merged {len(res) // NRUNS} cells from {merge_from}", flush=True)
     jobs = sorted([(k, r) for k in range(len(SIZES)) for r in range(NRUNS) if (k, r) not in res],
-                  key=lambda j: -SIZES[j[0]])
+                  key=lambda j: SIZES[j[0]] if args.reverse else -SIZES[j[0]])
     with Pool(args.jobs) as pool:
         for k, r, t8, ev, inp, out, sec in pool.imap_unordered(run, jobs):
             res[(k, r)] = (t8, ev, inp, out, sec)
