@@ -153,6 +153,13 @@ bool panel4_enabled() {
   const char* e = getenv("OI_PANEL4");
   return !(e && atoi(e) == 0);
 }
+// k_panel4 from even column OI_PANEL4_MINJ on (k_panel_even below it: with few
+// streamed pairs per workgroup the paired-row epilogue costs more than the
+// shared operand stream saves)
+int panel4_minj() {
+  const char* e = getenv("OI_PANEL4_MINJ");
+  return e ? atoi(e) : 0;
+}
 // Executed MFMA flops per cell and launch (profile mode), mirroring the
 // kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
 // 16-deep k-chunk is 8192 flops.  gemm2 (k_panel_even: 8 waves, wr 0..1,
@@ -518,7 +525,8 @@ struct Slot {
 class Engine {
  public:
   Engine(Context& ctx, const oi_options& o, int64_t cap_hint)
-      : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()), panel4_(panel4_enabled()) {
+      : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()), panel4_(panel4_enabled()),
+        panel4_minj_(panel4_minj()) {
     HIPC(hipSetDevice(ctx.device));
     st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
     ss_ = ctx.sub_stream;
@@ -915,7 +923,7 @@ class Engine {
       const bool empty_panel = j == maxT - 1 && ne == 0;
       if (empty_panel) {
       } else if (even) {
-        const int ke = panel4_ && !pform_ ? K_EVEN4 : K_EVEN;
+        const int ke = panel4_ && !pform_ && j >= panel4_minj_ ? K_EVEN4 : K_EVEN;
         mark(ke, false);
         if (ke == K_EVEN4)
           rc |= oi_launch_panel4(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
@@ -934,7 +942,7 @@ class Engine {
           if (pform_ && j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
           if (empty_panel)
             continue;
-          else if (even && panel4_ && !pform_)
+          else if (even && panel4_ && !pform_ && j >= panel4_minj_)
             kfl_[K_EVEN4] += acct::panel4(cd.T, cd.n, j, ev);
           else if (even)
             kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev, !pform_);
@@ -1077,6 +1085,7 @@ class Engine {
   Context& ctx_;
   oi_options o_;
   bool legacy_ = false, pform_ = false, poison_ = false, panel4_ = false;
+  int panel4_minj_ = 0;
   hipStream_t st_ = nullptr, ss_ = nullptr;
   hipEvent_t ready_ = nullptr;
   int cap_ = 1, G_ = 1, capG_ = 1;
