@@ -160,6 +160,14 @@ int panel4_minj() {
   const char* e = getenv("OI_PANEL4_MINJ");
   return e ? atoi(e) : 0;
 }
+// ... and only in rounds whose largest cell has at least OI_PANEL4_MINT (12)
+// block columns: on small cells (config 2, n = 500, T = 8: 271 k vs 284 k
+// cells/s; config 1) k_panel_even's one-tile workgroups finish sooner, on the
+// day (T up to 35) k_panel4 wins (138.1 vs 136.3 cells/s with it from j = 8 on)
+int panel4_mint() {
+  const char* e = getenv("OI_PANEL4_MINT");
+  return e ? atoi(e) : 12;
+}
 // Executed MFMA flops per cell and launch (profile mode), mirroring the
 // kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
 // 16-deep k-chunk is 8192 flops.  gemm2 (k_panel_even: 8 waves, wr 0..1,
@@ -526,7 +534,7 @@ class Engine {
  public:
   Engine(Context& ctx, const oi_options& o, int64_t cap_hint)
       : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()), panel4_(panel4_enabled()),
-        panel4_minj_(panel4_minj()) {
+        panel4_minj_(panel4_minj()), panel4_mint_(panel4_mint()) {
     HIPC(hipSetDevice(ctx.device));
     st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
     ss_ = ctx.sub_stream;
@@ -702,6 +710,10 @@ class Engine {
   }
 
   bool done(int64_t id) const { return id < next_id_ && !jobs_.count(id); }
+
+  bool use_panel4(int j, int maxT) const {
+    return panel4_ && !pform_ && j >= panel4_minj_ && maxT >= panel4_mint_;
+  }
 
   // The stream later submissions' device inputs are ordered after (the rounds
   // keep the stream chosen at construction).
@@ -923,7 +935,7 @@ class Engine {
       const bool empty_panel = j == maxT - 1 && ne == 0;
       if (empty_panel) {
       } else if (even) {
-        const int ke = panel4_ && !pform_ && j >= panel4_minj_ ? K_EVEN4 : K_EVEN;
+        const int ke = use_panel4(j, maxT) ? K_EVEN4 : K_EVEN;
         mark(ke, false);
         if (ke == K_EVEN4)
           rc |= oi_launch_panel4(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
@@ -942,7 +954,7 @@ class Engine {
           if (pform_ && j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
           if (empty_panel)
             continue;
-          else if (even && panel4_ && !pform_ && j >= panel4_minj_)
+          else if (even && use_panel4(j, maxT))
             kfl_[K_EVEN4] += acct::panel4(cd.T, cd.n, j, ev);
           else if (even)
             kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev, !pform_);
@@ -1085,7 +1097,7 @@ class Engine {
   Context& ctx_;
   oi_options o_;
   bool legacy_ = false, pform_ = false, poison_ = false, panel4_ = false;
-  int panel4_minj_ = 0;
+  int panel4_minj_ = 0, panel4_mint_ = 12;
   hipStream_t st_ = nullptr, ss_ = nullptr;
   hipEvent_t ready_ = nullptr;
   int cap_ = 1, G_ = 1, capG_ = 1;

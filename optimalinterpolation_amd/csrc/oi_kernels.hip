@@ -1360,19 +1360,25 @@ __device__ __forceinline__ void post_right4x2(const Quad8& acc, double* lds, con
   for (int kk = 0; kk < 8; ++kk) bA[kk] = kk <= 4 * nA + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * nA + fr) : 0.0;
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) bB[kk] = kk <= 4 * nB + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * nB + fr) : 0.0;
-  if (A0) {  // S_r += A_r: element (m, q) at q*64 + m, read coalesced (8 per thread and tile)
+  if (A0) {  // S_r += A_r: element (m, q) at q*64 + m, 8 per thread and tile.  A wave-
+    // instruction covers 32 rows m x 2 columns q (lane l: m = m0 + l/2, q = q0 + l%2):
+    // the global reads are two 256-B runs, and S[m*SLD + q] (bank 4m + 2q) hits 64
+    // distinct banks per 32-lane read and 32 per 16-lane write (2m + q distinct mod 16)
     double av[8], bv[8];
+    int ix[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      av[u] = gld(A0 + t + GEMM_THREADS * u);
-      bv[u] = two ? gld(A1 + t + GEMM_THREADS * u) : 0.0;
+      const int g = t + GEMM_THREADS * u, b = g >> 6, l = g & 63;
+      const int m = 32 * (b & 1) + (l >> 1), q = 2 * (b >> 1) + (l & 1);
+      ix[u] = m * SLD + q;
+      av[u] = gld(A0 + q * NB + m);
+      bv[u] = two ? gld(A1 + q * NB + m) : 0.0;
     }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int e = t + GEMM_THREADS * u, q = e >> 6, m = e & 63;
-      lds[m * SLD + q] += av[u];
-      if (two) lds[NB * SLD + m * SLD + q] += bv[u];
+      lds[ix[u]] += av[u];
+      if (two) lds[NB * SLD + ix[u]] += bv[u];
     }
   }
   __syncthreads();

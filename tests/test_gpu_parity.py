@@ -186,8 +186,8 @@ def test_panel_schemes_agree(scheme, monkeypatch):
         assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
 
 
-@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4'), ('OI_PFORM', '1'), ('OI_PANEL4', '1'),
-                                        ('OI_PANEL4', '0')])
+@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4'), ('OI_PFORM', '1'), ('OI_PANEL4', '0'),
+                                        ('OI_PANEL4_MINT', '0')])
 def test_alternate_kernels_agree(knob, value, monkeypatch):
     """The A/B alternates kept in the library -- round 1's 32-blocked diagonal
     factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r), the
@@ -328,6 +328,7 @@ def test_panel4_equals_panel_even(monkeypatch):
     mX = np.full(len(cells.z), cells.mean)
     hyp = np.tile(synthetic.FIXED_HYPERS, (len(sizes), 1))
     res = {}
+    monkeypatch.setenv('OI_PANEL4_MINT', '0')   # k_panel4 in every round (default: rounds with T >= 12)
     for p4 in ('0', '1'):
         for poison in ('0', '1'):
             monkeypatch.setenv('OI_PANEL4', p4)
