@@ -69,6 +69,9 @@ def parse():
                    help='day slices: equal-cost LPT mixes (lpt) or consecutive runs of the '
                         'largest-n-first order (ordered)')
     p.add_argument('--depth', type=int, default=8, help='slices in flight beyond the one waited on')
+    p.add_argument('--pregathered', action='store_true',
+                   help='day / season: submit each slice from pre-gathered per-cell inputs (round 2) instead of '
+                        'the radius query + gather over the pooled training set inside the timed region')
     p.add_argument('--max-pool', type=int, default=4096, help='max resident cells of the session (0: library default)')
     p.add_argument('--budget-s', type=float, default=420.0,
                    help='wall-clock budget from process start; stop submitting slices beyond it')
@@ -135,6 +138,45 @@ def split_slices(sizes, k, how='lpt', sites=None):
     cum = np.cumsum(costs[order])
     cut = np.searchsorted(cum, cum[-1] * np.arange(1, k) / k)
     return [np.sort(p) for p in np.split(order, cut)]
+
+
+POOL_PITCH_M = 1.0e6  # lattice pitch of the pooled training set (> 2 x (RADIUS_M + grid spacing))
+
+
+def pool_training_set(slices, grid_m, torch, dev):
+    """All timed cells as ONE training set resident in HBM, so that the radius
+    query and the gather of GPR:159-161 (oi_ball_query / oi_gather_rows) run
+    inside the timed region like the rest of GPR3D.  The synthetic day draws
+    each cell's observations on their own (n ~ U{300..3000}), so
+    the points the query searches are the observations translated cell by
+    cell -- cell g's centre onto node g of a 1000 km lattice, every one of its
+    observations by the same amount -- and no ball of radius RADIUS_M + grid_m
+    reaches another cell's points: the query returns exactly the cell's
+    observations in their original order.  The gathered columns are the
+    observations as drawn, so the fit sees bit-identical inputs (the Matérn
+    distances are formed from sqrt(3) x / ell, GPR:93, which is not exactly
+    translation invariant)."""
+    from optimalinterpolation_amd import synthetic
+    cols, sx, sy, q_all, g = [[], [], [], []], [], [], [], 0
+    for cells in slices:
+        q = np.empty((cells.ncell, 2))
+        for c in range(cells.ncell):
+            lx, ly = POOL_PITCH_M * (1 + g % 128), POOL_PITCH_M * (1 + g // 128)
+            a, b = cells.offs[c], cells.offs[c + 1]
+            x = cells.xyt[a:b]
+            for d in range(3):
+                cols[d].append(x[:, d])
+            cols[3].append(cells.z[a:b])
+            sx.append(x[:, 0] - cells.xs[c, 0] + lx)
+            sy.append(x[:, 1] - cells.xs[c, 1] + ly)
+            q[c] = lx, ly
+            g += 1
+        q_all.append(torch.from_numpy(q).to(dev))
+    cat = [np.concatenate(cc) if cc else np.zeros(0) for cc in cols]
+    dcols = tuple(torch.from_numpy(cc).to(dev).contiguous() for cc in cat)
+    pts = np.column_stack([np.concatenate(sx), np.concatenate(sy)]) if sx else np.zeros((0, 2))
+    return {"cols": dcols, "pts": torch.from_numpy(np.ascontiguousarray(pts)).to(dev), "q": q_all,
+            "r": synthetic.RADIUS_M + grid_m, "M": int(len(cat[0]))}
 
 
 def build_slices(args, rank, world):
@@ -750,6 +792,26 @@ def main():
         cells, xyt, z, h = item
         return sess.submit(xyt, z, cells.offs, cells.xs, cells.mean, x0=x0 if opt else None, opt=opt, hyp=h)
 
+    # day / season: the neighbour query and gather (GPR:159-161) inside the
+    # timed region, over the rank's cells pooled into one training set
+    pool = None
+    if args.workload in ('day', 'days', 'season') and not args.pregathered:
+        pool = pool_training_set(slices, synthetic.GRID_12P5_M if args.workload == 'season' else synthetic.GRID_M,
+                                 torch, dev)
+        cfg["neighbour_query"] = (f"inside the timed region: per slice oi_ball_query (r = {pool['r'] / 1e3:.0f} km) "
+                                  f"over the rank's {pool['M']} observations pooled into one HBM-resident training "
+                                  f"set, then oi_gather_rows (GPR:159-161); the searched positions are cell g's "
+                                  f"observations translated to node g of a {POOL_PITCH_M / 1e3:.0f} km lattice, "
+                                  f"the gathered columns the observations as drawn")
+
+    def submit_queried(sess, k):
+        cells = slices[k]
+        offs, idx = _lib.ball_query_device(pool['pts'], pool['q'][k], pool['r'])
+        if not np.array_equal(offs, cells.offs):
+            raise RuntimeError(f"slice {k}: the radius query returned other observations than the cells' own")
+        xyt, z = _lib.gather_rows_device(pool['cols'], idx)
+        return sess.submit(xyt, z, cells.offs, cells.xs, cells.mean, x0=x0, opt=True)
+
     # library initialisation (context, arena, code objects): one untimed
     # one-shot call on 8 small cells -- not a step
     if not args.no_prime:
@@ -767,6 +829,8 @@ def main():
         for item in dev_warm:
             submit(sess, item)
         sess.wait(-1)
+        if pool is not None:  # the query / gather code paths, untimed
+            _lib.gather_rows_device(pool['cols'], _lib.ball_query_device(pool['pts'], pool['q'][0], pool['r'])[1])
     prof_untimed = _lib.profile_json()['kernels']  # priming + warmup launches (rocprof sees them too)
     _lib.profile_reset()
     log("warmup done; timing")
@@ -786,7 +850,7 @@ def main():
             outs[k] = _lib.gpr_batch_device(xyt, z, cells.offs, cells.xs, cells.mean, x0=X0, opt=True,
                                             info=True, device=gpu, profile=False)
         else:
-            tickets.append(submit(sess, item))
+            tickets.append(submit_queried(sess, k) if pool is not None else submit(sess, item))
             if k >= args.depth:
                 outs[k - args.depth] = sess.wait(tickets[k - args.depth])
         done_k = k + 1

@@ -41,15 +41,19 @@ struct HipErr {
     if (e_ != hipSuccess) throw HipErr{std::string(#expr) + ": " + hipGetErrorString(e_)}; \
   } while (0)
 
-// device buffer owned for the duration of one call
+// device buffer owned for the duration of one call, allocated and freed in
+// the call's stream order: hipFree would synchronise the whole device, so a
+// radius query issued between a session's rounds (bench.py's timed day) would
+// drain the rounds in flight on the session's streams
 struct DBuf {
   void* p = nullptr;
+  hipStream_t s = nullptr;
   DBuf() = default;
-  explicit DBuf(size_t bytes) {
-    if (bytes) HC(hipMalloc(&p, bytes));
+  DBuf(size_t bytes, hipStream_t st) : s(st) {
+    if (bytes) HC(hipMallocAsync(&p, bytes, s));
   }
   ~DBuf() {
-    if (p) (void)hipFree(p);
+    if (p) (void)hipFreeAsync(p, s);
   }
   DBuf(const DBuf&) = delete;
   DBuf& operator=(const DBuf&) = delete;
@@ -128,7 +132,7 @@ int oi_smooth_fields(const double* fields, int32_t nf, int64_t ny, int64_t nx, c
   if (int rc = setup(opts, c)) return rc;
   return guarded([&] {
     const size_t npix = (size_t)ny * nx, fb = (size_t)nf * npix * 8;
-    DBuf dk(kv.size() * 8), dv((size_t)nf * 8);
+    DBuf dk(kv.size() * 8, c.s), dv((size_t)nf * 8, c.s);
     HC(hipMemcpyAsync(dk.p, kv.data(), kv.size() * 8, hipMemcpyHostToDevice, c.s));
     HC(hipMemcpyAsync(dv.p, vmax, (size_t)nf * 8, hipMemcpyHostToDevice, c.s));
     if (c.o.device_inputs) {
@@ -137,7 +141,7 @@ int oi_smooth_fields(const double* fields, int32_t nf, int64_t ny, int64_t nx, c
       HC(hipStreamSynchronize(c.s));
       return 0;
     }
-    DBuf din(fb), dout(fb), dm(npix * 8);
+    DBuf din(fb, c.s), dout(fb, c.s), dm(npix * 8, c.s);
     HC(hipMemcpyAsync(din.p, fields, fb, hipMemcpyHostToDevice, c.s));
     HC(hipMemcpyAsync(dm.p, mask, npix * 8, hipMemcpyHostToDevice, c.s));
     if (oi_launch_smooth(din.as<double>(), dout.as<double>(), nf, ny, nx, dv.as<double>(),
@@ -162,14 +166,14 @@ int oi_ball_query(const double* pts, int64_t M, const double* q, int64_t Q, doub
   return guarded([&] {
     const double r2 = r * r;
     const bool dev = c.o.device_inputs != 0;
-    DBuf dpts(dev ? 0 : (size_t)M * 16), dq(dev ? 0 : (size_t)Q * 16);
+    DBuf dpts(dev ? 0 : (size_t)M * 16, c.s), dq(dev ? 0 : (size_t)Q * 16, c.s);
     const double* P = dev ? pts : dpts.as<double>();
     const double* Qp = dev ? q : dq.as<double>();
     if (!dev) {
       if (M) HC(hipMemcpyAsync(dpts.p, pts, (size_t)M * 16, hipMemcpyHostToDevice, c.s));
       HC(hipMemcpyAsync(dq.p, q, (size_t)Q * 16, hipMemcpyHostToDevice, c.s));
     }
-    DBuf bbox((size_t)((M + 255) / 256 + 1) * 32), cnt((size_t)Q * 8);
+    DBuf bbox((size_t)((M + 255) / 256 + 1) * 32, c.s), cnt((size_t)Q * 8, c.s);
     if (oi_launch_ball_count(P, M, bbox.as<double>(), Qp, Q, r2, cnt.as<int64_t>(), c.s))
       throw HipErr{"ball count launch failed"};
     std::vector<int64_t> h((size_t)Q);
@@ -178,9 +182,9 @@ int oi_ball_query(const double* pts, int64_t M, const double* q, int64_t Q, doub
     for (int64_t k = 0; k < Q; ++k) offs[k + 1] = offs[k] + h[(size_t)k];
     const int64_t total = offs[Q];
     if (!idx || total > cap || total == 0) return 0;  // caller sizes idx from offs[Q]
-    DBuf doffs((size_t)(Q + 1) * 8);
+    DBuf doffs((size_t)(Q + 1) * 8, c.s);
     HC(hipMemcpyAsync(doffs.p, offs, (size_t)(Q + 1) * 8, hipMemcpyHostToDevice, c.s));
-    DBuf didx(dev ? 0 : (size_t)total * 8);
+    DBuf didx(dev ? 0 : (size_t)total * 8, c.s);
     int64_t* I = dev ? idx : didx.as<int64_t>();
     if (oi_launch_ball_fill(P, M, bbox.as<double>(), Qp, Q, r2, doffs.as<int64_t>(), I, c.s))
       throw HipErr{"ball fill launch failed"};
@@ -208,8 +212,8 @@ int oi_gather_rows(const double* x_train, const double* y_train, const double* t
     }
     for (int64_t k = 0; k < N; ++k)
       if (idx[k] < 0 || idx[k] >= M) return oi_set_last_error(OI_E_ARG, "index out of range");
-    DBuf dx((size_t)M * 8), dy((size_t)M * 8), dt((size_t)M * 8), dz((size_t)M * 8),
-        di((size_t)N * 8), dxyt((size_t)N * 24), dzo((size_t)N * 8);
+    DBuf dx((size_t)M * 8, c.s), dy((size_t)M * 8, c.s), dt((size_t)M * 8, c.s), dz((size_t)M * 8, c.s),
+        di((size_t)N * 8, c.s), dxyt((size_t)N * 24, c.s), dzo((size_t)N * 8, c.s);
     HC(hipMemcpyAsync(dx.p, x_train, (size_t)M * 8, hipMemcpyHostToDevice, c.s));
     HC(hipMemcpyAsync(dy.p, y_train, (size_t)M * 8, hipMemcpyHostToDevice, c.s));
     HC(hipMemcpyAsync(dt.p, t_train, (size_t)M * 8, hipMemcpyHostToDevice, c.s));

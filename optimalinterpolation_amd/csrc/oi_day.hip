@@ -232,20 +232,44 @@ __device__ __forceinline__ bool in_ball(const double* __restrict__ pts, int64_t 
   return d <= r2;
 }
 
+// The chunks a query's ball may touch, in ascending order, 256 at a time: every
+// thread tests one chunk's bounding box and the hits are compacted in order
+// into LDS (wave ballots + wave prefix), so a workgroup walks nchunk / 256
+// batches instead of testing every chunk serially.  Returns the batch's count.
+__device__ __forceinline__ int chunk_batch(const double* __restrict__ bbox, int64_t nchunk, int64_t base,
+                                           double qx, double qy, double r2, int* list, int* wcnt) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t ch = base + t;
+  const bool may = ch < nchunk && chunk_may_hit(bbox + 4 * ch, qx, qy, r2);
+  const unsigned long long m = __ballot(may);
+  if (lane == 0) wcnt[w] = __popcll(m);
+  __syncthreads();
+  int before = 0;
+  for (int k = 0; k < w; ++k) before += wcnt[k];
+  if (may) list[before + __popcll(lane ? (m & ((1ull << lane) - 1ull)) : 0ull)] = t;
+  const int total = ((wcnt[0] + wcnt[1]) + wcnt[2]) + wcnt[3];
+  __syncthreads();
+  return total;
+}
+
 // one workgroup (256 threads = 4 waves) per query
 __global__ __launch_bounds__(256) void k_ball_count(const double* __restrict__ pts, int64_t M,
                                                     const double* __restrict__ bbox,
                                                     const double* __restrict__ q, double r2,
                                                     int64_t* __restrict__ counts) {
   __shared__ int64_t red[4];
+  __shared__ int list[BQ_CHUNK], wcnt[4];
   const double qx = q[2 * blockIdx.x], qy = q[2 * blockIdx.x + 1];
   const int64_t nchunk = (M + BQ_CHUNK - 1) / BQ_CHUNK;
   int64_t cnt = 0;
-  for (int64_t ch = 0; ch < nchunk; ++ch) {
-    if (!chunk_may_hit(bbox + 4 * ch, qx, qy, r2)) continue;
-    const int64_t i = ch * BQ_CHUNK + threadIdx.x;
-    const bool hit = i < M && in_ball(pts, i, qx, qy, r2);
-    cnt += __popcll(__ballot(hit));
+  for (int64_t base = 0; base < nchunk; base += BQ_CHUNK) {
+    const int nc = chunk_batch(bbox, nchunk, base, qx, qy, r2, list, wcnt);
+    for (int k = 0; k < nc; ++k) {
+      const int64_t i = (base + list[k]) * BQ_CHUNK + threadIdx.x;
+      const bool hit = i < M && in_ball(pts, i, qx, qy, r2);
+      cnt += __popcll(__ballot(hit));
+    }
+    __syncthreads();  // list is rewritten by the next batch
   }
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
   __syncthreads();
@@ -258,26 +282,29 @@ __global__ __launch_bounds__(256) void k_ball_fill(const double* __restrict__ pt
                                                    const int64_t* __restrict__ offs,
                                                    int64_t* __restrict__ idx) {
   __shared__ int wcnt[4];
+  __shared__ int list[BQ_CHUNK], bcnt[4];
   const double qx = q[2 * blockIdx.x], qy = q[2 * blockIdx.x + 1];
   const int64_t nchunk = (M + BQ_CHUNK - 1) / BQ_CHUNK;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int64_t pos = offs[blockIdx.x];
-  for (int64_t ch = 0; ch < nchunk; ++ch) {
-    if (!chunk_may_hit(bbox + 4 * ch, qx, qy, r2)) continue;
-    const int64_t i = ch * BQ_CHUNK + threadIdx.x;
-    const bool hit = i < M && in_ball(pts, i, qx, qy, r2);
-    const unsigned long long m = __ballot(hit);
-    if (lane == 0) wcnt[w] = __popcll(m);
-    __syncthreads();
-    int before = 0;
-    for (int k = 0; k < w; ++k) before += wcnt[k];
-    const int total = ((wcnt[0] + wcnt[1]) + wcnt[2]) + wcnt[3];
-    if (hit) {
-      const unsigned long long lt = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
-      idx[pos + before + __popcll(lt)] = i;
+  for (int64_t base = 0; base < nchunk; base += BQ_CHUNK) {
+    const int nc = chunk_batch(bbox, nchunk, base, qx, qy, r2, list, bcnt);
+    for (int k = 0; k < nc; ++k) {
+      const int64_t i = (base + list[k]) * BQ_CHUNK + threadIdx.x;
+      const bool hit = i < M && in_ball(pts, i, qx, qy, r2);
+      const unsigned long long m = __ballot(hit);
+      if (lane == 0) wcnt[w] = __popcll(m);
+      __syncthreads();
+      int before = 0;
+      for (int kk = 0; kk < w; ++kk) before += wcnt[kk];
+      const int total = ((wcnt[0] + wcnt[1]) + wcnt[2]) + wcnt[3];
+      if (hit) {
+        const unsigned long long lt = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
+        idx[pos + before + __popcll(lt)] = i;
+      }
+      pos += total;
+      __syncthreads();
     }
-    pos += total;
-    __syncthreads();
   }
 }
 

@@ -103,7 +103,10 @@ int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, in
                          int with_trtri, int pform, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                          void* stream);
-int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, void* stream);
+// flag != nullptr: the last workgroup stores seq to *flag (pinned host) once all
+// result rows are in host memory; *done (device, zero) counts finished cells
+int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, unsigned* done,
+                       unsigned long long* flag, unsigned long long seq, void* stream);
 // r[a] = y[a] - (mX ? mX[a] : 1.0 * mean)
 int oi_set_debug(int on);
 // Sites of every cell of a batch (one workgroup per cell): offs (device,

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -457,11 +458,11 @@ struct DBuf {
 struct HBuf {  // pinned host
   void* p = nullptr;
   size_t n = 0;
-  void reserve(size_t bytes) {
+  void reserve(size_t bytes, unsigned flags = hipHostMallocDefault) {
     if (bytes <= n) return;
     if (p) HIPC(hipHostFree(p));
     p = nullptr;
-    HIPC(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    HIPC(hipHostMalloc(&p, bytes, flags));
     n = bytes;
   }
   ~HBuf() {
@@ -561,9 +562,16 @@ class Engine {
     blk_ = ((size_t)capG_ * (sizeof(OiCell) + 4 * 3 + 4) + 255) & ~size_t(255);
     d_blk_.reserve(G_ * blk_);
     h_blk_.reserve(G_ * blk_);
-    d_res_.reserve(cap_ * OI_OUT_N * 8);
-    h_res_.reserve(cap_ * OI_OUT_N * 8);
+    // result rows and the per-group completion flags: fine-grained pinned host
+    // memory the kernels write directly (k_finalize), no D2H copy per round
+    h_res_.reserve(cap_ * OI_OUT_N * 8, hipHostMallocCoherent | hipHostMallocMapped);
     hres_ = (double*)h_res_.p;
+    HIPC(hipHostGetDevicePointer((void**)&dres_, hres_, 0));
+    h_flag_.reserve(G_ * 64, hipHostMallocCoherent | hipHostMallocMapped);
+    std::memset(h_flag_.p, 0, G_ * 64);
+    HIPC(hipHostGetDevicePointer((void**)&dflag_, h_flag_.p, 0));
+    d_done_.reserve(G_ * 64);
+    HIPC(hipMemset(d_done_.p, 0, G_ * 64));
     groups_.resize(G_);
     for (int g = 0; g < G_; ++g) {
       Group& gr = groups_[g];
@@ -762,6 +770,8 @@ class Engine {
     int32_t* hstat = nullptr;  // status words (cleared on the host every round)
     int32_t* dstat = nullptr;
     bool inflight = false;
+    bool flagged = false;         // completion by host flag (else stream synchronise)
+    unsigned long long seq = 0;   // rounds launched: the flag value of the latest
     int maxT = 0;
     std::vector<hipEvent_t> ev;
     std::vector<int> ev_kind;
@@ -820,7 +830,7 @@ class Engine {
       cd.xyt = job.sites + 3 * job.offs[c];
       cd.r = job.v + job.offs[c];
       cd.dw = job.dw + job.offs[c];
-      cd.out = (double*)d_res_.p + (size_t)s * OI_OUT_N;
+      cd.out = dres_ + (size_t)s * OI_OUT_N;
       cd.status = gr.dstat + (s - gr.s0);
       cd.n = (int32_t)n;
       cd.n_obs = (int32_t)(job.offs[c + 1] - job.offs[c]);
@@ -972,12 +982,15 @@ class Engine {
     mark(K_LAUUM, true);
     // nlZ / dnlZ of the fitting cells and fs / sd / lZ of the predicting ones
     cur_cells = na;
+    // the host spins on the group's flag (profiling rounds synchronise the
+    // stream: their events are read back)
+    const int g = (int)(&gr - groups_.data());
+    gr.flagged = !o_.profile && na > 0;
     mark(K_FINAL, false);
-    rc |= oi_launch_finalize(dc, dl_all, na, gst);
+    rc |= oi_launch_finalize(dc, dl_all, na, (unsigned*)d_done_.p + 16 * g,
+                             gr.flagged ? (unsigned long long*)(dflag_ + 64 * g) : nullptr, ++gr.seq, gst);
     mark(K_FINAL, true);
     if (rc) throw HipError(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    HIPC(hipMemcpyAsync(hres_ + (size_t)gr.s0 * OI_OUT_N, (double*)d_res_.p + (size_t)gr.s0 * OI_OUT_N,
-                        (size_t)gr.cap * OI_OUT_N * 8, hipMemcpyDeviceToHost, gst));
     if (o_.profile) {
       for (int k = 0; k < ne; ++k) {
         const OiCell& cd = hc(gr.ev_slots[k]);
@@ -988,9 +1001,33 @@ class Engine {
     launch_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
   }
 
+  // Wait for the group's round: spin on its host flag (k_finalize stores the
+  // round's sequence number after the last result row), checking the stream
+  // every ~1 ms so a failed launch surfaces as an error instead of a hang.
+  void wait_round(Group& gr) {
+    if (!gr.flagged) {
+      HIPC(hipStreamSynchronize(gr.st));
+      return;
+    }
+    const int g = (int)(&gr - groups_.data());
+    const volatile unsigned long long* f = (const volatile unsigned long long*)((char*)h_flag_.p + 64 * g);
+    auto last = std::chrono::steady_clock::now();
+    for (unsigned spin = 0; *f != gr.seq; ++spin) {
+      if ((spin & 1023u) != 0) continue;
+      const auto now = std::chrono::steady_clock::now();
+      if (now - last < std::chrono::milliseconds(1)) continue;
+      last = now;
+      const hipError_t e = hipStreamQuery(gr.st);
+      if (e == hipErrorNotReady) continue;
+      if (e != hipSuccess) throw HipError(std::string("round failed: ") + hipGetErrorString(e));
+      if (*f != gr.seq) throw HipError("round completed without its completion flag");
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
+
   void consume(Group& gr) {
     const auto ts0 = std::chrono::steady_clock::now();
-    HIPC(hipStreamSynchronize(gr.st));
+    wait_round(gr);
     sync_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts0).count();
     gr.inflight = false;
     ++rounds_;
@@ -1103,10 +1140,12 @@ class Engine {
   int cap_ = 1, G_ = 1, capG_ = 1;
   std::vector<Slot> slots_;
   std::vector<Group> groups_;
-  DBuf d_blk_, d_res_;
-  HBuf h_blk_, h_res_;
+  DBuf d_blk_, d_done_;
+  HBuf h_blk_, h_res_, h_flag_;
   size_t blk_ = 0;  // bytes of one group's round block
-  double* hres_ = nullptr;
+  double* hres_ = nullptr;  // result rows (host view)
+  double* dres_ = nullptr;  // the same rows, device view
+  char* dflag_ = nullptr;   // device view of h_flag_ (64 B per group)
   std::deque<std::pair<Job*, int64_t>> queue_;
   std::map<int64_t, std::unique_ptr<Job>> jobs_;
   int64_t next_id_ = 0;

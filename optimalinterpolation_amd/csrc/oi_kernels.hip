@@ -689,6 +689,243 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
   DIAG_STAMP(7);
 }
 
+// ------------------------------------------ k_diag_factor4w(j) (default since round 3)
+// The same contract as k_diag_factor16 on four waves with the tile in LDS, for
+// latency (config 1's lone cell waits for four of these per evaluation; the
+// single-wave kernel spent half its 60 k cycles outside the serial potrf, one
+// wave issuing every store, the dtrti2 broadcasts and the inverse levels):
+//   potrf: 16-column panels; wave 0 factors the panel (row per lane, column
+//          values by v_readlane), all four waves then apply the trailing
+//          update A_IK -= P_I P_K^T (I >= K > J) on v_mfma_f64_16x16x4f64;
+//   inverse: wave b inverts diagonal block b by forward substitution, one
+//          lane per column (L read by LDS broadcast), then the off-diagonal
+//          blocks Inv_IJ = -Inv_II sum_{K=J}^{I-1} L_IK Inv_KJ by levels
+//          I - J = 1, 2, 3, one block per wave;
+//   stores of L, Dinv and W by all 256 threads (coalesced columns).
+// LDS (77 KB, two workgroups per CU): As = the tile, then L (row-major, stride
+// 65, zero above the diagonal); Is = Inv (row-major, zero above); per-wave
+// 16 x 17 scratch; z_j / v_j.
+#define DW_LD 65
+// workgroup barrier that waits for this wave's LDS operations only: HIP's
+// __syncthreads() is a workgroup-scope release, which also waits for every
+// outstanding global store (vmcnt(0)) -- here the L / Dinv / W stores would
+// stall each following phase on HBM write latency.  The workgroup shares only
+// LDS data between phases; the "memory" clobber keeps the compiler from moving
+// memory operations across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict__ cells,
+                                                      const int32_t* __restrict__ list, int j) {
+  __shared__ double As[NB * DW_LD];
+  __shared__ double Is[NB * DW_LD];
+  __shared__ double Xs[4 * 16 * 17];
+  __shared__ double Vs[3 * NB];
+  __shared__ int bad;
+  const OiCell& c = cells[list[blockIdx.x]];
+  if (j >= c.T || *c.status != OI_OK) return;
+  DIAG_STAMP(0);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, fr = lane & 15, fk = lane >> 4;
+  const bool pred = c.mode == OI_MODE_PREDICT;
+  double* Y = tileL(c, j, j);
+  double* zj = c.vec + j * NB;
+  double* vj = c.vec + 3 * c.T * NB + j * NB;
+  // element (r, q) of the column-major tile at q*64 + r: 16 coalesced loads per
+  // thread; the upper triangle (scratch of k_build) is replaced by zeros
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + 256 * u, q = e >> 6, r = e & 63;
+    const double v = gld(Y + e);
+    As[r * DW_LD + q] = r >= q ? v : 0.0;
+    Is[r * DW_LD + q] = 0.0;
+  }
+  if (t < NB) {
+    Vs[t] = zj[t];
+    Vs[NB + t] = pred ? vj[t] : 0.0;
+  }
+  lds_barrier();
+  DIAG_STAMP(1);
+  // ---------------- potrf by 16-column panels
+  double dmin = __builtin_inf();  // smallest pivot (wave 0; minNum passes a NaN pivot over)
+#pragma unroll
+  for (int J = 0; J < 4; ++J) {
+    const int c0 = 16 * J;
+    if (w == 0) {
+      const int r = lane;
+      double R[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) R[q] = As[r * DW_LD + c0 + q];
+      // rows r < c0 + q compute values nobody reads (zeros are written back)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int cc = c0 + q;
+        const double d = rdlane(R[q], cc);
+        dmin = fmin(dmin, d);
+        // 1/sqrt(d) by v_rsq_f64 + two Newton steps (<= 1 ulp), as k_diag_factor16
+        double il = __builtin_amdgcn_rsq(d);
+        il = fma(0.5 * il, fma(-d * il, il, 1.0), il);
+        il = fma(0.5 * il, fma(-d * il, il, 1.0), il);
+        const double l = d * il;
+        const double qd = R[q] * il;
+        R[q] = r == cc ? l : qd;
+#pragma unroll
+        for (int s2 = q + 1; s2 < 16; ++s2) R[s2] -= qd * rdlane(R[q], c0 + s2);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) As[r * DW_LD + c0 + q] = r >= c0 + q ? R[q] : 0.0;
+    }
+    lds_barrier();
+    if (J == 3) break;
+    // trailing update A_IK -= P_I P_K^T for J < K <= I (P: the panel's rows),
+    // 6 / 3 / 1 blocks of 16 x 16 over the four waves; the diagonal blocks'
+    // upper halves are scratch until their panel writes zeros back
+    const int nblk = (3 - J) * (4 - J) / 2;
+    for (int b = w; b < nblk; b += 4) {
+      int I = J + 1, rem = b;
+      while (rem >= I - J) {
+        rem -= I - J;
+        ++I;
+      }
+      const int K = J + 1 + rem;
+      d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+      mfma16x16(acc, As + 16 * I * DW_LD + c0, DW_LD, false, As + 16 * K * DW_LD + c0, DW_LD);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) As[(16 * I + fk + 4 * q) * DW_LD + 16 * K + fr] -= acc[q];
+    }
+    lds_barrier();
+  }
+  DIAG_STAMP(2);
+  if (t == 0) bad = dmin <= 0.0;
+  lds_barrier();
+  if (bad) {
+    if (t == 0) {
+      *c.status = OI_NOT_PD;
+      if (g_debug)
+        printf("oi debug: not PD: cell n=%d T=%d diagonal tile j=%d hyp %g %g %g %g %g\n", c.n, c.T,
+               j, c.hyp[0], c.hyp[1], c.hyp[2], c.hyp[3], c.hyp[4]);
+    }
+    return;
+  }
+  // L_jj (column-major) and sum log L_rr
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + 256 * u, q = e >> 6, r = e & 63;
+    gst(Y + e, As[r * DW_LD + q]);
+  }
+  if (w == 0) {
+    double lg = (j * NB + lane < c.n) ? log(As[lane * (DW_LD + 1)]) : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
+    if (lane == 0) {
+      const int ntile = c.T * (c.T + 1) / 2;
+      c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
+    }
+  }
+  DIAG_STAMP(3);
+  // ---------------- inverse: diagonal block w by forward substitution, lane fr = column
+  {
+    // column fr of Inv_ww: x = L_ww^-1 e_fr, right-looking (x_i final once the
+    // columns before it are applied; the updates of later rows are independent),
+    // x_i scaled by 1/L_ii as LAPACK's dtrti2 does (lane i holds 1/L_ii)
+    const int o = 16 * w;
+    const double rl = 1.0 / As[(o + fr) * DW_LD + o + fr];
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = i == fr ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      x[i] *= rdlane(rl, i);  // rows above the column: exact zeros
+#pragma unroll
+      for (int k = i + 1; k < 16; ++k) x[k] -= As[(o + k) * DW_LD + o + i] * x[i];
+    }
+    if (fk == 0)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Is[(o + i) * DW_LD + o + fr] = x[i];
+  }
+  lds_barrier();
+  DIAG_STAMP(4);
+  // ---------------- off-diagonal blocks by levels (wave w: J = w, I = J + lev)
+  double* Xw = Xs + w * 272;
+#pragma unroll
+  for (int lev = 1; lev < 4; ++lev) {
+    const int Jb = w, Ib = w + lev;
+    const bool act = Ib < 4;
+    if (act) {
+      d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int K = Jb; K < Ib; ++K)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * kk + fk;
+          acc = MFMA64(As[(16 * Ib + fr) * DW_LD + 16 * K + k], Is[(16 * K + k) * DW_LD + 16 * Jb + fr], acc);
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xw[(fk + 4 * q) * 17 + fr] = acc[q];  // Xw[k][n] = X[k][n]
+    }
+    lds_barrier();
+    if (act) {
+      d4 y = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = 4 * kk + fk;
+        y = MFMA64(Is[(16 * Ib + fr) * DW_LD + 16 * Ib + k], Xw[k * 17 + fr], y);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Is[(16 * Ib + fk + 4 * q) * DW_LD + 16 * Jb + fr] = -y[q];
+    }
+    lds_barrier();
+  }
+  DIAG_STAMP(5);
+  // Dinv_jj column-major: D[q*64 + r] = Inv[r][q]
+  double* Dj = tileD(c, j);
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + 256 * u, q = e >> 6, r = e & 63;
+    gst(Dj + e, Is[r * DW_LD + q]);
+  }
+  // forward substitution, block j: z_j = Dinv_jj z_j (the panels subtracted the
+  // sum over k < j), v_j likewise for predict; z^T z, z^T v, v^T v partials
+  if (w == 0) {
+    double zp[4] = {0.0, 0.0, 0.0, 0.0}, vp[4] = {0.0, 0.0, 0.0, 0.0};  // four chains
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const double a = Is[lane * DW_LD + q];
+      zp[q & 3] = fma(a, Vs[q], zp[q & 3]);
+      vp[q & 3] = fma(a, Vs[NB + q], vp[q & 3]);
+    }
+    const double zn = (zp[0] + zp[1]) + (zp[2] + zp[3]), vn = (vp[0] + vp[1]) + (vp[2] + vp[3]);
+    gst(zj + lane, zn);
+    if (pred) gst(vj + lane, vn);
+    Vs[2 * NB + lane] = zn;
+    double zz = zn * zn, zv = zn * vn, vv = vn * vn;
+    for (int o = 32; o >= 1; o >>= 1) {
+      zz += __shfl_down(zz, o, 64);
+      zv += __shfl_down(zv, o, 64);
+      vv += __shfl_down(vv, o, 64);
+    }
+    if (lane == 0) {
+      double* pp = c.part + OI_PART_PRED(c.T * (c.T + 1) / 2, c.T) + 3 * j;
+      pp[0] = zz;
+      pp[1] = zv;
+      pp[2] = vv;
+    }
+  }
+  DIAG_STAMP(6);
+  if (c.mode == OI_MODE_EVAL) {
+    // W_jj row-major (W[q][r] = Inv[q][r]) and alpha_j = W_jj^T z_j
+    double* Wj = tileW(c, j, j);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u;
+      gst(Wj + e, Is[(e >> 6) * DW_LD + (e & 63)]);
+    }
+    lds_barrier();  // z_j in Vs
+    if (w == 0) {
+      double ap[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < NB; ++q) ap[q & 3] = fma(Is[q * DW_LD + lane], Vs[2 * NB + q], ap[q & 3]);
+      gst(c.vec + c.T * NB + j * NB + lane, (ap[0] + ap[1]) + (ap[2] + ap[3]));
+    }
+  }
+  DIAG_STAMP(7);
+}
+
 // ----------------------------------------------------------- k_scale(j)
 // P_jk = -Dinv_jj L_jk for k < j (column-major), so that the panel tiles and
 // the row of W become single GEMM loops (no separate Dinv product per tile).
@@ -1773,9 +2010,7 @@ void k_lauum_grad4(const OiCell* __restrict__ cells,
 
 // ---------------------------------------------------------- k_finalize
 // nlZ = r.alpha/2 + sum log diag L + n log(2 pi)/2 (GPR:128); dnlZ (GPR:131-138)
-__global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cells,
-                                                  const int32_t* __restrict__ list) {
-  const OiCell& c = cells[list[blockIdx.x]];
+__device__ __forceinline__ void finalize_cell(const OiCell& c) {
   __shared__ double red[4 * 7];
   const int t = threadIdx.x, T = c.T, ntile = T * (T + 1) / 2;
   // the round's status rides home in the result row (one D2H copy per round)
@@ -1829,6 +2064,27 @@ __global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cel
     c.out[4] = v[3] / 2;
     c.out[5] = sn2 * ((v[4] + nm / sn2) - c.ssw / (sn2 * sn2));
     c.out[6] = 0.0;
+  }
+}
+
+// The result rows live in fine-grained pinned host memory (no D2H copy per
+// round).  With `flag` set, the workgroup that finishes last stores `seq` to
+// the group's host flag after every row has reached host memory, and the host
+// spins on that word instead of a stream synchronise (config 1's lone cell
+// waits for ~90 of these round trips: 7 us spinning vs 12 us synchronising,
+// + 3 us for the copy, tools/sync_probe.hip).
+__global__ __launch_bounds__(256) void k_finalize(const OiCell* __restrict__ cells,
+                                                  const int32_t* __restrict__ list, unsigned* done,
+                                                  unsigned long long* flag, unsigned long long seq,
+                                                  int ncell) {
+  finalize_cell(cells[list[blockIdx.x]]);
+  if (flag == nullptr) return;
+  __threadfence_system();  // this thread's result stores are in host memory
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(done, 1u) == (unsigned)(ncell - 1)) {
+    *done = 0u;  // for the group's next round (stream order)
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1992,11 +2248,13 @@ extern "C" int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, i
                                      void* stream) {
   if (ncell <= 0) return 0;
   const char* ev = getenv("OI_DIAG");  // read per launch (tests switch it): ~0.1 us
-  const int variant = ev ? atoi(ev) : 16;
+  const int variant = ev ? atoi(ev) : 4;
   if (variant == 32)  // the round-1 32-blocked kernel (A/B)
     hipLaunchKernelGGL(k_diag_factor, dim3(ncell), dim3(64), 0, S(stream), cells, list, j);
-  else
+  else if (variant == 16)  // round 2's single-wave 16-blocked kernel (A/B)
     hipLaunchKernelGGL(k_diag_factor16, dim3(ncell), dim3(64), 0, S(stream), cells, list, j);
+  else
+    hipLaunchKernelGGL(k_diag_factor4w, dim3(ncell), dim3(256), 0, S(stream), cells, list, j);
   return ret();
 }
 
@@ -2061,10 +2319,10 @@ extern "C" int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, in
   return ret();
 }
 
-extern "C" int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell,
-                                  void* stream) {
+extern "C" int oi_launch_finalize(const OiCell* cells, const int32_t* list, int ncell, unsigned* done,
+                                  unsigned long long* flag, unsigned long long seq, void* stream) {
   if (ncell <= 0) return 0;
-  hipLaunchKernelGGL(k_finalize, dim3(ncell), dim3(256), 0, S(stream), cells, list);
+  hipLaunchKernelGGL(k_finalize, dim3(ncell), dim3(256), 0, S(stream), cells, list, done, flag, seq, ncell);
   return ret();
 }
 

@@ -91,6 +91,44 @@ def test_ball_query_edges():
         assert np.array_equal(idx[offs[c]:offs[c + 1]], D.ball_query(p, np.array(q), 3e5))
 
 
+def test_ball_query_many_chunk_batches():
+    """More than 256 chunks (the kernels prune chunk boxes 256 at a time):
+    index sets and order equal the oracle's on 200 000 points, queries whose
+    hits straddle batch boundaries and one that hits nothing."""
+    rng = np.random.default_rng(5)
+    p = rng.uniform(0.0, 4e6, (200_000, 2))
+    p[70_000:70_300] = rng.uniform(1e7, 1.01e7, (300, 2))   # a far-away clump inside batch 1
+    q = np.array([[2e6, 2e6], [1.0e7 + 5e3, 1.0e7 + 5e3], [3.9e6, 1e5], [-9e6, -9e6]])
+    offs, idx = _lib.ball_query(p, q, 2.5e5)
+    for c in range(len(q)):
+        assert np.array_equal(idx[offs[c]:offs[c + 1]], D.ball_query(p, q[c], 2.5e5)), c
+    assert offs[4] - offs[3] == 0 and offs[2] - offs[1] == 300
+
+
+def test_pooled_training_set_returns_each_cells_own_rows():
+    """bench.py's in-region query: the rank's cells pooled into one training
+    set on a lattice; the device query + gather must hand every cell exactly
+    its drawn observations, in order (the searched positions are translated
+    copies, the gathered columns the drawn values), so the fit equals the
+    pre-gathered submission bitwise."""
+    import torch
+    import bench
+    cells = synthetic.make_cells([300, 420, 310, 505, 333], seed=3)
+    slices = [cells.subset([0, 1, 2]), cells.subset([3, 4])]
+    pool = bench.pool_training_set(slices, synthetic.GRID_M, torch, torch.device('cuda', 0))
+    outs = []
+    for k, sl in enumerate(slices):
+        offs, idx = _lib.ball_query_device(pool['pts'], pool['q'][k], pool['r'])
+        assert np.array_equal(offs, sl.offs)
+        xyt, z = _lib.gather_rows_device(pool['cols'], idx)
+        assert np.array_equal(xyt.cpu().numpy(), sl.xyt) and np.array_equal(z.cpu().numpy(), sl.z)
+        a = _lib.gpr_batch_device(xyt, z, sl.offs, sl.xs, sl.mean, x0=bench.X0, opt=True, device=0)
+        b = _lib.gpr_batch(sl.xyt, sl.z, sl.offs, sl.xs, sl.mean, x0=bench.X0, opt=True)
+        outs.append((a[0], b[0]))
+    for a, b in outs:
+        assert np.array_equal(a, b)
+
+
 def test_gather_rejects_bad_index():
     with pytest.raises(_lib.OiError):
         _lib.gather_rows(np.zeros(3), np.zeros(3), np.zeros(3), np.zeros(3), np.array([0, 3]))

@@ -186,11 +186,12 @@ def test_panel_schemes_agree(scheme, monkeypatch):
         assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
 
 
-@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_LAUUM', '4'), ('OI_PFORM', '1'), ('OI_PANEL4', '0'),
+@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_DIAG', '16'), ('OI_LAUUM', '4'), ('OI_PFORM', '1'), ('OI_PANEL4', '0'),
                                         ('OI_PANEL4_MINT', '0')])
 def test_alternate_kernels_agree(knob, value, monkeypatch):
     """The A/B alternates kept in the library -- round 1's 32-blocked diagonal
-    factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r), the
+    factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r), round 2's
+    single-wave 16-blocked one (OI_DIAG=16; the default is the 4-wave kernel), the
     128x128 K^-1 / gradient kernel (OI_LAUUM=4) and the P-form panels
     (OI_PFORM=1: k_scale's P_jk = -Dinv_jj L_jk streamed by the panels, both
     panel schemes) -- meet the T1 tolerance on tile-boundary sizes, fit and

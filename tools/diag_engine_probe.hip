@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
     int32_t s0 = -1;
     CHK(hipMemcpy(&s0, status, 4, hipMemcpyDeviceToHost));
     printf("engine k_diag_factor%s B=%5d: p50 %8.2f us/launch (min %.2f) status %d\n",
-           getenv("OI_DIAG") ? getenv("OI_DIAG") : "16", B, v[v.size() / 2], v[0], s0);
+           getenv("OI_DIAG") ? getenv("OI_DIAG") : "4w", B, v[v.size() / 2], v[0], s0);
   }
   return 0;
 }
