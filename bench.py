@@ -685,6 +685,7 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
     fam_alg = {'factor': float(np.sum((evals * 2.0 / 3.0 + 1.0 / 3.0) * n ** 3)),
                'lauum': float(np.sum(evals * n ** 3 / 3.0))}
     fam_of = {'k_scale': 'factor', 'k_panel_even': 'factor', 'k_panel4': 'factor', 'k_chol_panel': 'factor',
+              'k_panel_pair': 'factor',
               'k_lauum_grad': 'lauum'}
     fam = fam_of.get(dom)
     fam_exec = sum(v['flops'] for k, v in kern.items() if fam_of.get(k) == fam) if fam else 0.0

@@ -55,7 +55,8 @@ struct OiCell {
   double* L;          // packed lower tiles (T(T+1)/2 * 4096)
   double* W;          // packed lower tiles of L^-1 (eval mode), else null
   double* Dinv;       // T * 4096
-  double* P;          // T * 4096: P_jk = -Dinv_jj L_jk of the current block column (P-form only, else null)
+  double* P;          // P-form: T * 4096, P_jk = -Dinv_jj L_jk of the current block column; folded pair
+                      // step: 4 * 4096 scratch (E tiles 0..2, W_j+1,j column-major in tile 3)
   double* vec;        // 4 * T * 64: z | alpha | kstar | v.  z = L^-1 r and (predict)
                       // v = L^-1 k* are built in place during the factorisation
   double* part;       // partial sums, see OI_PART_*
@@ -101,6 +102,12 @@ int oi_launch_panel4(const OiCell* cells, const int32_t* list, int ncell, int ma
                      void* stream);
 int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
                          int with_trtri, int pform, void* stream);
+// folded pair step (OI_FOLD=1): k_diag_pair(j) factors / inverts the 128 x 128
+// diagonal block (j, j+1); k_panel_pair(j) finishes both block columns (c.P: 4
+// scratch tiles per cell)
+int oi_launch_diag_pair(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
+int oi_launch_panel_pair(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j, int with_trtri,
+                         void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                          void* stream);
 // flag != nullptr: the last workgroup stores seq to *flag (pinned host) once all

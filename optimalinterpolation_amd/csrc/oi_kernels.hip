@@ -713,38 +713,13 @@ __global__ __launch_bounds__(64) void k_diag_factor16(const OiCell* __restrict__
 // LDS data between phases; the "memory" clobber keeps the compiler from moving
 // memory operations across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict__ cells,
-                                                      const int32_t* __restrict__ list, int j) {
-  __shared__ double As[NB * DW_LD];
-  __shared__ double Is[NB * DW_LD];
-  __shared__ double Xs[4 * 16 * 17];
-  __shared__ double Vs[3 * NB];
-  __shared__ int bad;
-  const OiCell& c = cells[list[blockIdx.x]];
-  if (j >= c.T || *c.status != OI_OK) return;
-  DIAG_STAMP(0);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, fr = lane & 15, fk = lane >> 4;
-  const bool pred = c.mode == OI_MODE_PREDICT;
-  double* Y = tileL(c, j, j);
-  double* zj = c.vec + j * NB;
-  double* vj = c.vec + 3 * c.T * NB + j * NB;
-  // element (r, q) of the column-major tile at q*64 + r: 16 coalesced loads per
-  // thread; the upper triangle (scratch of k_build) is replaced by zeros
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int e = t + 256 * u, q = e >> 6, r = e & 63;
-    const double v = gld(Y + e);
-    As[r * DW_LD + q] = r >= q ? v : 0.0;
-    Is[r * DW_LD + q] = 0.0;
-  }
-  if (t < NB) {
-    Vs[t] = zj[t];
-    Vs[NB + t] = pred ? vj[t] : 0.0;
-  }
-  lds_barrier();
-  DIAG_STAMP(1);
-  // ---------------- potrf by 16-column panels
-  double dmin = __builtin_inf();  // smallest pivot (wave 0; minNum passes a NaN pivot over)
+// potrf of the 64 x 64 tile in As (row-major, stride DW_LD, lower triangle; the
+// upper triangle is scratch) on four waves, As <- L with zeros above the
+// diagonal.  Returns the smallest pivot in wave 0 (+inf in the other waves;
+// minNum passes a NaN pivot over, as the reference's cholesky does).
+__device__ __forceinline__ double potrf4w(double* As) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = lane >> 4;
+  double dmin = __builtin_inf();
 #pragma unroll
   for (int J = 0; J < 4; ++J) {
     const int c0 = 16 * J;
@@ -792,34 +767,13 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
     }
     lds_barrier();
   }
-  DIAG_STAMP(2);
-  if (t == 0) bad = dmin <= 0.0;
-  lds_barrier();
-  if (bad) {
-    if (t == 0) {
-      *c.status = OI_NOT_PD;
-      if (g_debug)
-        printf("oi debug: not PD: cell n=%d T=%d diagonal tile j=%d hyp %g %g %g %g %g\n", c.n, c.T,
-               j, c.hyp[0], c.hyp[1], c.hyp[2], c.hyp[3], c.hyp[4]);
-    }
-    return;
-  }
-  // L_jj (column-major) and sum log L_rr
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int e = t + 256 * u, q = e >> 6, r = e & 63;
-    gst(Y + e, As[r * DW_LD + q]);
-  }
-  if (w == 0) {
-    double lg = (j * NB + lane < c.n) ? log(As[lane * (DW_LD + 1)]) : 0.0;
-    for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
-    if (lane == 0) {
-      const int ntile = c.T * (c.T + 1) / 2;
-      c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
-    }
-  }
-  DIAG_STAMP(3);
-  // ---------------- inverse: diagonal block w by forward substitution, lane fr = column
+  return dmin;
+}
+
+// Is <- L^-1 of the factored tile in As (row-major, stride DW_LD); Is must
+// hold zeros in its blocks above the diagonal.  Xs: 4 x 16 x 17 scratch.
+__device__ __forceinline__ void trtri4w(const double* As, double* Is, double* Xs) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = lane >> 4;
   {
     // column fr of Inv_ww: x = L_ww^-1 e_fr, right-looking (x_i final once the
     // columns before it are applied; the updates of later rows are independent),
@@ -871,6 +825,67 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
     }
     lds_barrier();
   }
+}
+
+__global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict__ cells,
+                                                      const int32_t* __restrict__ list, int j) {
+  __shared__ double As[NB * DW_LD];
+  __shared__ double Is[NB * DW_LD];
+  __shared__ double Xs[4 * 16 * 17];
+  __shared__ double Vs[3 * NB];
+  __shared__ int bad;
+  const OiCell& c = cells[list[blockIdx.x]];
+  if (j >= c.T || *c.status != OI_OK) return;
+  DIAG_STAMP(0);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const bool pred = c.mode == OI_MODE_PREDICT;
+  double* Y = tileL(c, j, j);
+  double* zj = c.vec + j * NB;
+  double* vj = c.vec + 3 * c.T * NB + j * NB;
+  // element (r, q) of the column-major tile at q*64 + r: 16 coalesced loads per
+  // thread; the upper triangle (scratch of k_build) is replaced by zeros
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + 256 * u, q = e >> 6, r = e & 63;
+    const double v = gld(Y + e);
+    As[r * DW_LD + q] = r >= q ? v : 0.0;
+    Is[r * DW_LD + q] = 0.0;
+  }
+  if (t < NB) {
+    Vs[t] = zj[t];
+    Vs[NB + t] = pred ? vj[t] : 0.0;
+  }
+  lds_barrier();
+  DIAG_STAMP(1);
+  const double dmin = potrf4w(As);  // smallest pivot (wave 0)
+  DIAG_STAMP(2);
+  if (t == 0) bad = dmin <= 0.0;
+  lds_barrier();
+  if (bad) {
+    if (t == 0) {
+      *c.status = OI_NOT_PD;
+      if (g_debug)
+        printf("oi debug: not PD: cell n=%d T=%d diagonal tile j=%d hyp %g %g %g %g %g\n", c.n, c.T,
+               j, c.hyp[0], c.hyp[1], c.hyp[2], c.hyp[3], c.hyp[4]);
+    }
+    return;
+  }
+  // L_jj (column-major) and sum log L_rr
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + 256 * u, q = e >> 6, r = e & 63;
+    gst(Y + e, As[r * DW_LD + q]);
+  }
+  if (w == 0) {
+    double lg = (j * NB + lane < c.n) ? log(As[lane * (DW_LD + 1)]) : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
+    if (lane == 0) {
+      const int ntile = c.T * (c.T + 1) / 2;
+      c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
+    }
+  }
+  DIAG_STAMP(3);
+  trtri4w(As, Is, Xs);
   DIAG_STAMP(5);
   // Dinv_jj column-major: D[q*64 + r] = Inv[r][q]
   double* Dj = tileD(c, j);
@@ -924,6 +939,317 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
     }
   }
   DIAG_STAMP(7);
+}
+
+// ------------------------------------------------ k_diag_pair(j), j even
+// Folded pair step (OI_FOLD=1, default): the 128 x 128 diagonal block
+// JJ = (j, j+1) of a cell -- tile j alone when j + 1 = T -- is factored and
+// inverted in one launch, so that k_panel_pair(j) finishes BOTH block columns of
+// every row below it (no odd-column launch).  On entry the block holds
+//   A_JJ - sum_{k<j-2} L_Jk L_Jk^T   (k_panel_pair(j-2)'s look-ahead slot, in place)
+// and c.P tiles 0..2 hold E = sum_{k=j-2}^{j-1} L_Jk L_Jk^T for (j,j), (j+1,j),
+// (j+1,j+1) (its first row-pair workgroup; j >= 2 only).  Steps:
+//   L_jj = potrf(A'_jj - E_jj), Dinv_j = L_jj^-1        (potrf4w / trtri4w)
+//   L_j+1,j = (A'_j+1,j - E_j+1,j) Dinv_j^T
+//   L_j+1,j+1 = potrf(A'_j+1,j+1 - E_j+1,j+1 - L_j+1,j L_j+1,j^T), Dinv_j+1
+//   W_j+1,j = -Dinv_j+1 (L_j+1,j Dinv_j)   (the off-diagonal block of Winv_JJ;
+//            column-major copy in c.P tile 3 for the panel epilogue, row-major in W)
+//   z_j = Dinv_j z_j, z_j+1 = Dinv_j+1 (z_j+1 - L_j+1,j z_j)  (v likewise, predict)
+//   alpha_j = W_jj^T z_j + W_j+1,j^T z_j+1, alpha_j+1 = W_j+1,j+1^T z_j+1  (eval)
+// Scratch X = L_j+1,j Dinv_j goes through c.P tile 3 (the workgroup's own
+// global stores, ordered by __syncthreads): As / Is are the only tile buffers in
+// LDS, so two workgroups still fit a CU.
+__global__ __launch_bounds__(256) void k_diag_pair(const OiCell* __restrict__ cells,
+                                                  const int32_t* __restrict__ list, int j) {
+  __shared__ double As[NB * DW_LD];
+  __shared__ double Is[NB * DW_LD];
+  __shared__ double Xs[4 * 16 * 17];
+  __shared__ double Vs[7 * NB];  // z_j v_j zf_j | z_j+1 v_j+1 vf_j zf_j+1
+  __shared__ int bad;
+  const OiCell& c = cells[list[blockIdx.x]];
+  const int T = c.T;
+  if (j >= T || *c.status != OI_OK) return;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, fr = lane & 15, fk = lane >> 4;
+  const bool pred = c.mode == OI_MODE_PREDICT, eval = c.mode == OI_MODE_EVAL;
+  const bool pair = j + 1 < T, ext = j >= 2;
+  const int ntile = T * (T + 1) / 2;
+  double* z = c.vec;
+  double* al = c.vec + T * NB;
+  double* v = c.vec + 3 * T * NB;
+  const double* E = c.P;
+  double* W10c = c.P + 3 * OI_TILE;
+  double* pp = c.part + OI_PART_PRED(ntile, T);
+  double* lgd = c.part + OI_PART_LOGDET(ntile, T);
+  auto fail = [&](int jt) {
+    if (t == 0) {
+      *c.status = OI_NOT_PD;
+      if (g_debug)
+        printf("oi debug: not PD: cell n=%d T=%d diagonal tile j=%d hyp %g %g %g %g %g\n", c.n, T, jt,
+               c.hyp[0], c.hyp[1], c.hyp[2], c.hyp[3], c.hyp[4]);
+    }
+  };
+  auto logdet = [&](int jt) {  // wave 0: sum log L_rr of the factored tile in As
+    double lg = (jt * NB + lane < c.n) ? log(As[lane * (DW_LD + 1)]) : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
+    if (lane == 0) lgd[jt] = lg;
+  };
+  // ---- tile (j, j)
+  {
+    const double* Y = tileL(c, j, j);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      const double x = gld(Y + e) - (ext ? gld(E + e) : 0.0);
+      As[r * DW_LD + q] = r >= q ? x : 0.0;
+      Is[r * DW_LD + q] = 0.0;
+    }
+  }
+  if (t < NB) {
+    Vs[t] = z[j * NB + t];
+    Vs[NB + t] = pred ? v[j * NB + t] : 0.0;
+    Vs[3 * NB + t] = pair ? z[(j + 1) * NB + t] : 0.0;
+    Vs[4 * NB + t] = pair && pred ? v[(j + 1) * NB + t] : 0.0;
+  }
+  lds_barrier();
+  double dmin = potrf4w(As);
+  if (t == 0) bad = dmin <= 0.0;
+  lds_barrier();
+  if (bad) return fail(j);
+  {
+    double* Y = tileL(c, j, j);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      gst(Y + e, As[r * DW_LD + q]);
+    }
+  }
+  if (w == 0) logdet(j);
+  trtri4w(As, Is, Xs);
+  {
+    double* Dj = tileD(c, j);
+    double* Wj = eval ? tileW(c, j, j) : nullptr;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      gst(Dj + e, Is[r * DW_LD + q]);                     // column-major
+      if (eval) gst(Wj + e, Is[(e >> 6) * DW_LD + (e & 63)]);  // row-major
+    }
+  }
+  // z_j = Dinv_j z_j (v_j likewise), partial dot products of block j
+  if (w == 0) {
+    double zp[4] = {0.0, 0.0, 0.0, 0.0}, vp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const double a = Is[lane * DW_LD + q];
+      zp[q & 3] = fma(a, Vs[q], zp[q & 3]);
+      vp[q & 3] = fma(a, Vs[NB + q], vp[q & 3]);
+    }
+    const double zn = (zp[0] + zp[1]) + (zp[2] + zp[3]), vn = (vp[0] + vp[1]) + (vp[2] + vp[3]);
+    gst(z + j * NB + lane, zn);
+    if (pred) gst(v + j * NB + lane, vn);
+    Vs[2 * NB + lane] = zn;
+    Vs[5 * NB + lane] = vn;
+    double zz = zn * zn, zv = zn * vn, vv = vn * vn;
+    for (int o = 32; o >= 1; o >>= 1) {
+      zz += __shfl_down(zz, o, 64);
+      zv += __shfl_down(zv, o, 64);
+      vv += __shfl_down(vv, o, 64);
+    }
+    if (lane == 0) {
+      pp[3 * j] = zz;
+      pp[3 * j + 1] = zv;
+      pp[3 * j + 2] = vv;
+    }
+  }
+  lds_barrier();
+  double a_j = 0.0;  // wave 0: alpha_j[lane], W_jj^T z_j part
+  if (eval && w == 0) {
+    double ap[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NB; ++q) ap[q & 3] = fma(Is[q * DW_LD + lane], Vs[2 * NB + q], ap[q & 3]);
+    a_j = (ap[0] + ap[1]) + (ap[2] + ap[3]);
+    if (!pair) gst(al + j * NB + lane, a_j);
+  }
+  if (!pair) return;
+  // ---- L_j+1,j = A'_j+1,j Dinv_j^T (A' row-major in As; wave w: row block w)
+  {
+    const double* Y = tileL(c, j + 1, j);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      As[r * DW_LD + q] = gld(Y + e) - (ext ? gld(E + OI_TILE + e) : 0.0);
+    }
+  }
+  lds_barrier();
+  {
+    d4 o[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      o[nb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)  // B(q, n) = Dinv_j[n][q]: zero for q > n
+        if (kk <= 4 * nb + 3)
+          o[nb] = MFMA64(As[(16 * w + fr) * DW_LD + 4 * kk + fk], Is[(16 * nb + fr) * DW_LD + 4 * kk + fk], o[nb]);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) As[(16 * w + fk + 4 * r) * DW_LD + 16 * nb + fr] = o[nb][r];
+  }
+  lds_barrier();
+  {
+    double* Y = tileL(c, j + 1, j);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      gst(Y + e, As[r * DW_LD + q]);
+    }
+  }
+  // z_j+1 -= L_j+1,j z_j (wave 0), v_j+1 -= L_j+1,j v_j (wave 1, predict)
+  if (w == 0 || (w == 1 && pred)) {
+    const double* u = Vs + (w == 0 ? 2 : 5) * NB;
+    double sp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NB; ++q) sp[q & 3] = fma(As[lane * DW_LD + q], u[q], sp[q & 3]);
+    Vs[(w == 0 ? 3 : 4) * NB + lane] -= (sp[0] + sp[1]) + (sp[2] + sp[3]);
+  }
+  // syrk S = L_j+1,j L_j+1,j^T (lower 16x16 blocks w, w+4, w+8) and X = L_j+1,j Dinv_j
+  d4 sb[3], xo[4];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    sb[s] = (d4){0.0, 0.0, 0.0, 0.0};
+    const int b = w + 4 * s;
+    if (b < 10) {
+      const int bm = b >= 6 ? 3 : b >= 3 ? 2 : b >= 1 ? 1 : 0, bn = b - bm * (bm + 1) / 2;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+        sb[s] = MFMA64(As[(16 * bm + fr) * DW_LD + 4 * kk + fk], As[(16 * bn + fr) * DW_LD + 4 * kk + fk], sb[s]);
+    }
+  }
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    xo[nb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)  // B(q, n) = Dinv_j[q][n]: zero for q < n
+      if (kk >= 4 * nb)
+        xo[nb] = MFMA64(As[(16 * w + fr) * DW_LD + 4 * kk + fk], Is[(4 * kk + fk) * DW_LD + 16 * nb + fr], xo[nb]);
+  }
+  // X row-major into c.P tile 3 (read back below as the B operand, then replaced by W_j+1,j)
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gst(W10c + (16 * w + fk + 4 * r) * NB + 16 * nb + fr, xo[nb][r]);
+  lds_barrier();  // As / Is reads done, Vs updates visible
+  // ---- tile (j+1, j+1): A'_j+1,j+1 - E - S
+  {
+    const double* Y = tileL(c, j + 1, j + 1);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      const double x = gld(Y + e) - (ext ? gld(E + 2 * OI_TILE + e) : 0.0);
+      As[r * DW_LD + q] = r >= q ? x : 0.0;
+      Is[r * DW_LD + q] = 0.0;
+    }
+  }
+  lds_barrier();
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int b = w + 4 * s;
+    if (b < 10) {
+      const int bm = b >= 6 ? 3 : b >= 3 ? 2 : b >= 1 ? 1 : 0, bn = b - bm * (bm + 1) / 2;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) As[(16 * bm + fk + 4 * r) * DW_LD + 16 * bn + fr] -= sb[s][r];
+    }
+  }
+  lds_barrier();
+  dmin = potrf4w(As);
+  if (t == 0) bad = dmin <= 0.0;
+  lds_barrier();
+  if (bad) return fail(j + 1);
+  {
+    double* Y = tileL(c, j + 1, j + 1);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      gst(Y + e, As[r * DW_LD + q]);
+    }
+  }
+  if (w == 0) logdet(j + 1);
+  trtri4w(As, Is, Xs);
+  {
+    double* Dj = tileD(c, j + 1);
+    double* Wj = eval ? tileW(c, j + 1, j + 1) : nullptr;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      gst(Dj + e, Is[r * DW_LD + q]);
+      if (eval) gst(Wj + e, Is[(e >> 6) * DW_LD + (e & 63)]);
+    }
+  }
+  // z_j+1 = Dinv_j+1 z_j+1 (v likewise), partial dot products of block j+1
+  if (w == 0) {
+    double zp[4] = {0.0, 0.0, 0.0, 0.0}, vp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const double a = Is[lane * DW_LD + q];
+      zp[q & 3] = fma(a, Vs[3 * NB + q], zp[q & 3]);
+      vp[q & 3] = fma(a, Vs[4 * NB + q], vp[q & 3]);
+    }
+    const double zn = (zp[0] + zp[1]) + (zp[2] + zp[3]), vn = (vp[0] + vp[1]) + (vp[2] + vp[3]);
+    gst(z + (j + 1) * NB + lane, zn);
+    if (pred) gst(v + (j + 1) * NB + lane, vn);
+    Vs[6 * NB + lane] = zn;
+    double zz = zn * zn, zv = zn * vn, vv = vn * vn;
+    for (int o = 32; o >= 1; o >>= 1) {
+      zz += __shfl_down(zz, o, 64);
+      zv += __shfl_down(zv, o, 64);
+      vv += __shfl_down(vv, o, 64);
+    }
+    if (lane == 0) {
+      pp[3 * j + 3] = zz;
+      pp[3 * j + 4] = zv;
+      pp[3 * j + 5] = vv;
+    }
+  }
+  __syncthreads();  // X (global, this workgroup's stores) and z_j+1 complete
+  // W_j+1,j = -Dinv_j+1 X: A(m, q) = Inv[m][q] (zero for q > m), B(q, n) = X[q][n]
+  d4 wo[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    wo[nb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+      if (kk <= 4 * w + 3)
+        wo[nb] = MFMA64(Is[(16 * w + fr) * DW_LD + 4 * kk + fk], gld(W10c + (4 * kk + fk) * NB + 16 * nb + fr),
+                        wo[nb]);
+  }
+  __syncthreads();  // every read of X is done; As (L_j+1,j+1, stored) is free
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) As[(16 * w + fk + 4 * r) * DW_LD + 16 * nb + fr] = -wo[nb][r];
+  lds_barrier();
+  {
+    double* Wt = eval ? tileW(c, j + 1, j) : nullptr;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u;
+      gst(W10c + e, As[(e & 63) * DW_LD + (e >> 6)]);       // column-major: [n*64 + m] = W[m][n]
+      if (eval) gst(Wt + e, As[(e >> 6) * DW_LD + (e & 63)]);  // row-major
+    }
+  }
+  if (eval && w == 0) {
+    double ap[4] = {0.0, 0.0, 0.0, 0.0}, bp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const double zq = Vs[6 * NB + q];
+      ap[q & 3] = fma(As[q * DW_LD + lane], zq, ap[q & 3]);
+      bp[q & 3] = fma(Is[q * DW_LD + lane], zq, bp[q & 3]);
+    }
+    gst(al + j * NB + lane, a_j + ((ap[0] + ap[1]) + (ap[2] + ap[3])));
+    gst(al + (j + 1) * NB + lane, (bp[0] + bp[1]) + (bp[2] + bp[3]));
+  }
 }
 
 // ----------------------------------------------------------- k_scale(j)
@@ -1782,6 +2108,376 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
   alpha_update<GEMM_THREADS>(c, lds, XLD, jj2, apre2, lds + NB * XLD);
 }
 
+// --------------------------------------------------- k_panel_pair(j), j even
+// Folded pair step (OI_FOLD=1, default): with the whole 128 x 128 diagonal
+// block JJ = (j, j+1) factored and inverted by k_diag_pair(j), Winv_JJ =
+// [[Dinv_j, 0], [W_j+1,j, Dinv_j+1]], one stream per row pair finishes BOTH
+// block columns -- there is no odd-column launch (k_chol_panel) and no partial
+// update of column j+1 goes through HBM:
+//   [L_ij  L_i,j+1] = (A_iJ - sum_{k<j} L_ik L_Jk^T) Winv_JJ^T          (i >= j+2)
+//   [W_j,jj  ; W_j+1,jj] = -Winv_JJ sum_{k<j} L_Jk W_k,jj                 (jj < j)
+// Slots of a cell (gemm4 core, 512 threads, two 64-row outputs per workgroup):
+//   x < lead (= 1 if j >= 2): look-ahead of the next diagonal block J' = (j+2, j+3):
+//        A_J'J' -= sum_{k<j} L_J'k L_J'k^T (lower quadrants, in place)
+//   next nrp = ceil((T-2-j)/2): rows i1 = j+2+2y, i2 = i1+1; the first pair
+//        (rows J') then also forms E = sum_{k=j}^{j+1} L_J'k L_J'k^T into c.P
+//        tiles 0..2 for k_diag_pair(j+2) -- the two products the look-ahead
+//        slot cannot see, as their tiles are made in this launch
+//   then (eval) W column pairs jj1 = 2y', jj2 = jj1+1 < j.
+// Epilogue per output row r (64 x 128): S_r = A - acc staged row-major in LDS
+// (stride SLD2), out = S_r Winv_JJ^T on the MFMA unit, B fragments of Winv read
+// from L2 (Dinv tiles and W_j+1,j's column-major copy in c.P tile 3); the
+// accumulators of row 1 leave through their destination tiles in HBM (A - acc)
+// while row 0 is processed, since LDS holds one staged row and the registers
+// one accumulator set.
+#define SLD2 130  // (4m + 2q) mod 64: the 32-lane halves of a ds_read_b64 hit distinct banks
+static_assert(NB * SLD2 <= GEMM4_LDS && 2 * NB * XLD + 768 <= GEMM4_LDS, "panel-pair staging must fit");
+__host__ __device__ inline int npair_rows(int T, int j) { return T - 1 - j > 0 ? (T - 1 - j) >> 1 : 0; }
+
+// column blocks of a wave's share of the 128-wide triangular product: rows
+// 16 (w & 3) .. +16 against {0, 7, 2, 5} (w < 4) or {1, 6, 3, 4}: 72 k-steps each
+__device__ __forceinline__ int pair_nb(int h, int u) {
+  return h ? (u == 0 ? 1 : u == 1 ? 6 : u == 2 ? 3 : 4) : (u == 0 ? 0 : u == 1 ? 7 : u == 2 ? 2 : 5);
+}
+
+// B(q, n) = Winv_JJ[n][q], every part column-major ([q*64 + n]); callers ask only q <= n|15
+__device__ __forceinline__ double winv_frag(const double* D0, const double* W10, const double* D1, int n, int q) {
+  if (n < NB) return gld(D0 + q * NB + n);
+  if (q < NB) return gld(W10 + q * NB + (n - NB));
+  return gld(D1 + (q - NB) * NB + (n - NB));
+}
+
+// o[u] = (S Winv^T) block (w & 3, pair_nb(w >> 2, u)), S staged at S[m*SLD2 + q]; two = false:
+// the second block column is absent (columns 64..127 not formed).  The B
+// fragments come from L2 in groups of four k-steps, the next group in flight
+// while the current one's MFMAs run (the loop is kept rolled: register budget).
+__device__ __forceinline__ void post_pair(const double* S, const double* D0, const double* W10, const double* D1,
+                                          bool two, d4 (&o)[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = lane >> 4;
+  const int mb = w & 3, h = w >> 2;
+  const double* Srow = S + (16 * mb + fr) * SLD2 + fk;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    o[u] = (d4){0.0, 0.0, 0.0, 0.0};
+    const int nb = pair_nb(h, u);
+#ifdef OI_PP_NOEPI  // timing experiment only (scripts/build_exp_lib.sh): no triangular product
+    continue;
+#endif
+    if (!two && nb >= 4) continue;
+    const int ng = nb + 1, n = 16 * nb + fr;  // groups of 4 k-steps: q < 16 nb + 16
+    double b[4], bn[4];
+#pragma unroll
+    for (int kq = 0; kq < 4; ++kq) b[kq] = winv_frag(D0, W10, D1, n, 4 * kq + fk);
+#pragma unroll 1
+    for (int g = 0; g < ng; ++g) {
+      const int gn = g + 1 < ng ? g + 1 : g;  // the last prefetch re-reads the group
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) bn[kq] = winv_frag(D0, W10, D1, n, 16 * gn + 4 * kq + fk);
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) o[u] = MFMA64(Srow[16 * g + 4 * kq], b[kq], o[u]);
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) b[kq] = bn[kq];
+    }
+  }
+}
+
+// S[m*SLD2 + q] (op)= tile[q*64 + m] for a column-major 64 x 64 tile into columns
+// c0 .. c0+63 of the staged row (coalesced 256 B runs; add = false: assign)
+__device__ __forceinline__ void stage_tile_rm(double* S, int c0, const double* tile, bool add) {
+  const int t = threadIdx.x;
+  double av[8];
+  int ix[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int g = t + GEMM_THREADS * u, b = g >> 6, l = g & 63;
+    const int m = 32 * (b & 1) + (l >> 1), q = 2 * (b >> 1) + (l & 1);
+    ix[u] = m * SLD2 + c0 + q;
+    av[u] = gld(tile + q * NB + m);
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (add)
+      S[ix[u]] += av[u];
+    else
+      S[ix[u]] = av[u];
+  }
+}
+
+// quadrant (qr, qc) of a gemm4 accumulator staged as X[n*XLD + m] (emit_copy's layout)
+__device__ __forceinline__ void stage4_q(const Quad8& acc, int qr, int qc, double* X) {
+  const int w = threadIdx.x >> 6;
+  if ((w >> 2) == qr && (w & 1) == qc) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          X[(acc4_col(nb) - 64 * qc) * XLD + (acc4_row(mb, r) - 64 * qr)] = acc.c[mb][nb][r];
+  }
+}
+
+// y_d[m] = pre_d + sign * sum_{n<ncol} X[n*XLD + m] u_d[n] for d = 0 and (two) d = 1:
+// the forward substitution z_i -= L_iJ z_J (v likewise) of a finished factor
+// row, or alpha_jj += W_J,jj^T z_J of a finished W row.  Threads t < 256: row
+// m = t & 63, column group t >> 6; partial sums combined in a fixed order.
+// vec_preload (issued before the epilogue's products) gives thread t: u = u0[t]
+// (t < 128) / u1[t - 128], y = y0[t] (t < 64) / y1[t - 64] (t < 128).
+struct VecPre {
+  double u, y;
+};
+__device__ __forceinline__ VecPre vec_preload(const double* u0, const double* u1, const double* y0, const double* y1,
+                                              int ncol) {
+  const int t = threadIdx.x;
+  VecPre p = {0.0, 0.0};
+  if (t < ncol) p.u = u0[t];
+  else if (u1 && t >= 128 && t - 128 < ncol) p.u = u1[t - 128];
+  if (t < 64) p.y = y0[t];
+  else if (y1 && t < 128) p.y = y1[t - 64];
+  return p;
+}
+__device__ __forceinline__ void vec_update(const double* X, int ncol, bool two, VecPre p, double* y0, double* y1,
+                                           double sign, double* scratch) {
+  double* uu = scratch;         // 2 x 128
+  double* red = scratch + 256;  // 2 x 4 x 64
+  const int t = threadIdx.x;
+  if (t < 256) uu[t] = p.u;
+  __syncthreads();
+  if (t < 256) {
+    const int m = t & 63, g = t >> 6, cw = ncol >> 2;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll 4
+    for (int q = 0; q < cw; ++q) {
+      const int n = g * cw + q;
+      const double x = X[n * XLD + m];
+      s0 = fma(x, uu[n], s0);
+      if (two) s1 = fma(x, uu[128 + n], s1);
+    }
+    red[g * 64 + m] = s0;
+    red[256 + g * 64 + m] = s1;
+  }
+  __syncthreads();
+  if (t < 64 || (two && t < 128)) {
+    const int m = t & 63, d = t >> 6;
+    const double* rd = red + 256 * d;
+    const double a = (rd[m] + rd[64 + m]) + (rd[128 + m] + rd[192 + m]);
+    gst((d ? y1 : y0) + m, p.y + sign * a);
+  }
+}
+
+// One output row of a pair workgroup: S (staged) -> out = S Winv^T -> dst0 (columns of
+// block j) / dst1 (block j+1, if two) and the vector update.  Leaves LDS free.
+__device__ __forceinline__ void pair_row_out(double* lds, const double* D0, const double* W10, const double* D1,
+                                             bool two, double* dst0, double* dst1, VecPre p, bool two_vec,
+                                             double* y0, double* y1, double sign) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15;
+  const int mb = w & 3, h = w >> 2;
+  d4 o[4];
+  post_pair(lds, D0, W10, D1, two, o);
+  __syncthreads();  // S is read; its space takes the result
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int nb = pair_nb(h, u);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lds[(16 * nb + fr) * XLD + 16 * mb + (lane >> 4) + 4 * r] = o[u][r];
+  }
+  __syncthreads();
+  emit_copy(lds, dst0, EMIT_STORE);
+  if (two) emit_copy(lds + NB * XLD, dst1, EMIT_STORE);
+  vec_update(lds, two ? 2 * NB : NB, two_vec, p, y0, y1, sign, lds + 2 * NB * XLD);
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(GEMM_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_panel_pair(const OiCell* __restrict__ cells, const int32_t* __restrict__ list, int j, int gx, int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM4_LDS];
+  int ci, x;
+  if (!xcd_cell_slot(gx, ncell, ci, x)) return;
+  const OiCell& c = cells[list[ci]];
+  const int T = c.T;
+  if (j >= T || *c.status != OI_OK) return;
+  const int lead = j >= 2 ? 1 : 0, nrp = npair_rows(T, j);
+  const bool has_next = j + 1 < T, pred = c.mode == OI_MODE_PREDICT;
+  const int rT = c.n - NB * (T - 1);
+  const int t = threadIdx.x, w = t >> 6, wr = w >> 1, wc = w & 1;
+  const double* D0 = tileD(c, j);
+  const double* D1 = has_next ? tileD(c, j + 1) : nullptr;
+  const double* W10 = c.P + 3 * OI_TILE;
+  double* z = c.vec;
+  double* v = c.vec + 3 * T * NB;
+  Quad8 acc;
+  quad8_zero(acc);
+  if (x < lead) {
+    // ---- look-ahead: A_J'J' -= sum_{k<j} L_J'k L_J'k^T, J' = (j+2, j+3)
+    const int a = j + 2, b = j + 3;
+    if (a >= T) return;
+#ifdef OI_PP_NOLA  // timing experiment only: no look-ahead workgroup
+    return;
+#endif
+    const bool two = b < T;
+    unsigned skip = 0;
+    const int qr = wr >> 1;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int m0 = 32 * (wr & 1) + 16 * mb, n0 = 16 * nb, ti = qr ? b : a, tj = wc ? b : a;
+        const bool off = (qr == 0 && wc == 1) || ti >= T || tj >= T || (qr == wc && m0 + 15 < n0) ||
+                         (ti == T - 1 && m0 >= rT) || (tj == T - 1 && n0 >= rT);
+        if (off) skip |= 1u << (4 * mb + nb);
+      }
+    gemm4_kmajor<true>(acc, lds, 4 * j, skip, [=, &c](int p, const double*& a0, const double*& a1,
+                                                       const double*& b0, const double*& b1) {
+      a0 = tileL(c, a, p);
+      a1 = two ? tileL(c, b, p) : g_zero_tile;
+      b0 = a0;
+      b1 = a1;
+    });
+    __syncthreads();
+    stage4_q(acc, 0, 0, lds);
+    if (two) stage4_q(acc, 1, 0, lds + NB * XLD);
+    __syncthreads();
+    emit_copy(lds, tileL(c, a, a), EMIT_SUB);
+    if (!two) return;
+    emit_copy(lds + NB * XLD, tileL(c, b, a), EMIT_SUB);
+    __syncthreads();
+    stage4_q(acc, 1, 1, lds);
+    __syncthreads();
+    emit_copy(lds, tileL(c, b, b), EMIT_SUB);
+    return;
+  }
+  if (x < lead + nrp) {
+    // ---- rows i1, i2 of both block columns j, j+1 (j+1 < T here)
+    const int y = x - lead, i1 = j + 2 + 2 * y, i2 = i1 + 1;
+    const bool two = i2 < T;
+    unsigned skip = 0;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int m0 = 32 * (wr & 1) + 16 * mb, n0 = 16 * nb, ti = wr >= 2 ? i2 : i1, tj = wc ? j + 1 : j;
+        if (ti >= T || (ti == T - 1 && m0 >= rT) || (tj == T - 1 && n0 >= rT)) skip |= 1u << (4 * mb + nb);
+      }
+    auto fpair = [=, &c](int p, const double*& a0, const double*& a1, const double*& b0, const double*& b1) {
+      a0 = tileL(c, i1, p);
+      a1 = two ? tileL(c, i2, p) : g_zero_tile;
+      b0 = tileL(c, j, p);
+      b1 = tileL(c, j + 1, p);
+    };
+    if (i2 >= T - 1 || j + 1 == T - 1)
+      gemm4_kmajor<true>(acc, lds, 4 * j, skip, fpair);
+    else
+      gemm4_kmajor<false>(acc, lds, 4 * j, 0u, fpair);
+    __syncthreads();  // the GEMM's last LDS reads are done
+    if (two) {  // row i2 leaves through its tiles: A - acc
+      stage4_q(acc, 1, 0, lds);
+      stage4_q(acc, 1, 1, lds + NB * XLD);
+      __syncthreads();
+      emit_copy(lds, tileL(c, i2, j), EMIT_SUB);
+      emit_copy(lds + NB * XLD, tileL(c, i2, j + 1), EMIT_SUB);
+      __syncthreads();
+    }
+    if ((w >> 2) == 0) {  // S_1 = -acc of row i1, then + A
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) lds[acc4_row(mb, r) * SLD2 + acc4_col(nb)] = -acc.c[mb][nb][r];
+    }
+    __syncthreads();
+    stage_tile_rm(lds, 0, tileL(c, i1, j), true);
+    stage_tile_rm(lds, NB, tileL(c, i1, j + 1), true);
+    VecPre p = vec_preload(z + j * NB, pred ? v + j * NB : nullptr, z + i1 * NB, pred ? v + i1 * NB : nullptr, 2 * NB);
+    __syncthreads();
+    pair_row_out(lds, D0, W10, D1, true, tileL(c, i1, j), tileL(c, i1, j + 1), p, pred, z + i1 * NB,
+                 pred ? v + i1 * NB : nullptr, -1.0);
+    if (two) {
+      stage_tile_rm(lds, 0, tileL(c, i2, j), false);
+      stage_tile_rm(lds, NB, tileL(c, i2, j + 1), false);
+      p = vec_preload(z + j * NB, pred ? v + j * NB : nullptr, z + i2 * NB, pred ? v + i2 * NB : nullptr, 2 * NB);
+      __syncthreads();
+      pair_row_out(lds, D0, W10, D1, true, tileL(c, i2, j), tileL(c, i2, j + 1), p, pred, z + i2 * NB,
+                   pred ? v + i2 * NB : nullptr, -1.0);
+    }
+    if (y != 0) return;
+    // ---- E = sum_{k=j}^{j+1} L_J'k L_J'k^T for k_diag_pair(j+2), J' = (i1, i2), from the
+    // tiles just stored (this workgroup's own global stores, ordered by __syncthreads)
+    quad8_zero(acc);
+    gemm4_kmajor<false>(acc, lds, 8, 0u, [=, &c](int p, const double*& a0, const double*& a1, const double*& b0,
+                                                 const double*& b1) {
+      a0 = tileL(c, i1, j + p);
+      a1 = two ? tileL(c, i2, j + p) : g_zero_tile;
+      b0 = a0;
+      b1 = a1;
+    });
+    __syncthreads();
+    double* E = c.P;
+    stage4_q(acc, 0, 0, lds);
+    if (two) stage4_q(acc, 1, 0, lds + NB * XLD);
+    __syncthreads();
+    emit_copy(lds, E, EMIT_STORE);
+    if (!two) return;
+    emit_copy(lds + NB * XLD, E + OI_TILE, EMIT_STORE);
+    __syncthreads();
+    stage4_q(acc, 1, 1, lds);
+    __syncthreads();
+    emit_copy(lds, E + 2 * OI_TILE, EMIT_STORE);
+    return;
+  }
+  // ---- rows j, j+1 of W for the column pair jj1, jj2 (eval)
+  const int yw = x - lead - nrp;
+  if (c.mode != OI_MODE_EVAL || 2 * yw >= j) return;
+  const int jj1 = 2 * yw, jj2 = jj1 + 1;
+  unsigned skip = 0;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const int tj = wc ? j + 1 : j;
+      if ((wc == 1 && !has_next) || (tj == T - 1 && 16 * nb >= rT)) skip |= 1u << (4 * mb + nb);
+    }
+  auto wpair = [=, &c](int p, const double*& a0, const double*& a1, const double*& b0, const double*& b1) {
+    const int k = jj1 + p;
+    a0 = tileW(c, k, jj1);
+    a1 = k >= jj2 ? tileW(c, k, jj2) : g_zero_tile;
+    b0 = tileL(c, j, k);
+    b1 = has_next ? tileL(c, j + 1, k) : g_zero_tile;
+  };
+  if (j >= T - 2)
+    gemm4_kmajor<true>(acc, lds, 4 * (j - jj1), skip, wpair);
+  else
+    gemm4_kmajor<false>(acc, lds, 4 * (j - jj1), 0u, wpair);
+  __syncthreads();
+  // row jj2 leaves through its tiles: -acc
+  stage4_q(acc, 1, 0, lds);
+  if (has_next) stage4_q(acc, 1, 1, lds + NB * XLD);
+  __syncthreads();
+  emit_copy(lds, tileW(c, j, jj2), EMIT_NEG);
+  if (has_next) emit_copy(lds + NB * XLD, tileW(c, j + 1, jj2), EMIT_NEG);
+  __syncthreads();
+  if ((w >> 2) == 0) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds[acc4_row(mb, r) * SLD2 + acc4_col(nb)] = -acc.c[mb][nb][r];
+  }
+  double* al = c.vec + T * NB;
+  const int ncol = has_next ? 2 * NB : NB;
+  VecPre p = vec_preload(z + j * NB, nullptr, al + jj1 * NB, nullptr, ncol);
+  __syncthreads();
+  pair_row_out(lds, D0, W10, D1, has_next, tileW(c, j, jj1), has_next ? tileW(c, j + 1, jj1) : nullptr, p, false,
+               al + jj1 * NB, nullptr, 1.0);
+  stage_tile_rm(lds, 0, tileW(c, j, jj2), false);
+  if (has_next) stage_tile_rm(lds, NB, tileW(c, j + 1, jj2), false);
+  p = vec_preload(z + j * NB, nullptr, al + jj2 * NB, nullptr, ncol);
+  __syncthreads();
+  pair_row_out(lds, D0, W10, D1, has_next, tileW(c, j, jj2), has_next ? tileW(c, j + 1, jj2) : nullptr, p, false,
+               al + jj2 * NB, nullptr, 1.0);
+}
+
 // ------------------------------------------------------ k_lauum_grad
 // Tile (i, j) of K^-1 = W^T W (K^-1_ij = sum_{k>=i} W_ki^T W_kj), one 256-thread
 // workgroup per lower tile (40 KiB LDS -> 4 workgroups per CU), fused with
@@ -2298,6 +2994,21 @@ extern "C" int oi_launch_panel4(const OiCell* cells, const int32_t* list, int nc
   const int gx = nslot4_factor(maxT, j) + (with_trtri ? j / 2 : 0);
   if (ncell <= 0 || gx <= 0) return 0;
   hipLaunchKernelGGL(k_panel4, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j, gx,
+                     ncell);
+  return ret();
+}
+
+extern "C" int oi_launch_diag_pair(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream) {
+  if (ncell <= 0) return 0;
+  hipLaunchKernelGGL(k_diag_pair, dim3(ncell), dim3(256), 0, S(stream), cells, list, j);
+  return ret();
+}
+
+extern "C" int oi_launch_panel_pair(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
+                                    int with_trtri, void* stream) {
+  const int gx = (j >= 2 ? 1 : 0) + npair_rows(maxT, j) + (with_trtri ? j / 2 : 0);
+  if (ncell <= 0 || gx <= 0) return 0;
+  hipLaunchKernelGGL(k_panel_pair, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j, gx,
                      ncell);
   return ret();
 }

@@ -12,6 +12,16 @@ GOLDEN = os.path.join(ROOT, 'tests', 'golden')
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
+    # pytest-xdist workers: one BLAS thread each.  Several workers each running
+    # a full OpenBLAS thread pool on the same CPUs turn the oracle's many small
+    # solves into spin-wait contention (test_cg_trace_bitwise: 4.5 s alone,
+    # 640 s under -n 4); results are bitwise the same either way.
+    if os.environ.get('PYTEST_XDIST_WORKER'):
+        try:
+            from threadpoolctl import threadpool_limits
+            threadpool_limits(1)
+        except ImportError:
+            pass
 
 
 def load_golden(name):
