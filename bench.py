@@ -939,6 +939,9 @@ def main():
                 "rocprofv3 --kernel-trace --stats run of this command averages over"}
     if done_k != args.steps or truncated:
         line.update({"truncated": True, "steps_requested": args.steps})
+    if args.dump and rank == 0:  # per (kernel, block column) launch totals of the profiled pass
+        with open(args.dump + '.byj.json', 'w') as fh:
+            json.dump(prof.get('by_j', []), fh)
     if args.dump:
         np.savez(args.dump if rank == 0 else f"{args.dump}.rank{rank}.npz", n=sizes_timed, m=sites_timed,
                  evals=info[:, 3], nit=info[:, 0], cg_status=info[:, 1], status=status)

@@ -430,6 +430,14 @@ struct LaunchRec {
   double ms;
 };
 std::vector<LaunchRec> g_last_round;  // per-launch times of the latest profiled round
+// per (kernel, block column j) totals over every profiled round: launches,
+// resident cells, HIP-event ms, executed MFMA flops (the launch-shape analysis
+// of DESIGN §6: how much time goes to launches with few cells left at large j)
+struct ByJ {
+  int64_t launches = 0, cells = 0;
+  double ms = 0.0, flops = 0.0;
+};
+std::map<std::pair<int, int>, ByJ> g_byj;
 struct RoundRec {
   int n_eval, n_pred, maxT;
   double work;  // sum over evaluated cells of T^3
@@ -1050,14 +1058,14 @@ class Engine {
           const OiCell& cd = hc(all_slots[k]);
           const bool ev = cd.mode == OI_MODE_EVAL;
           if (pform_ && j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
-          if (empty_panel)
-            continue;
-          else if (even && use_panel4(j, maxT))
-            kfl_[K_EVEN4] += acct::panel4(cd.T, cd.n, j, ev);
-          else if (even)
-            kfl_[K_EVEN] += acct::panel_even(cd.T, cd.n, j, ev, !pform_);
-          else
-            kfl_[K_TRSM] += acct::chol_panel(cd.T, cd.n, j, kbeg, ev, !pform_);
+          if (empty_panel) continue;
+          const int kk = even ? (use_panel4(j, maxT) ? K_EVEN4 : K_EVEN) : K_TRSM;
+          const double f = kk == K_EVEN4 ? acct::panel4(cd.T, cd.n, j, ev)
+                           : kk == K_EVEN ? acct::panel_even(cd.T, cd.n, j, ev, !pform_)
+                                          : acct::chol_panel(cd.T, cd.n, j, kbeg, ev, !pform_);
+          kfl_[kk] += f;
+          std::lock_guard<std::mutex> pl(g_prof_mu);
+          g_byj[{kk, j}].flops += f;
         }
       }
     }
@@ -1127,6 +1135,15 @@ class Engine {
         kms_[gr.ev_kind[q]] += a;
         kln_[gr.ev_kind[q]]++;
         recs.push_back({gr.ev_kind[q], gr.ev_meta[q].first, gr.ev_meta[q].second, (double)a});
+      }
+      {
+        std::lock_guard<std::mutex> pl(g_prof_mu);
+        for (const auto& rr : recs) {
+          ByJ& b = g_byj[{rr.kind, rr.j}];
+          b.launches++;
+          b.cells += rr.cells;
+          b.ms += rr.ms;
+        }
       }
       double rms = 0.0, work = 0.0;
       for (const auto& rr : recs) rms += rr.ms;
@@ -1506,6 +1523,17 @@ int64_t oi_profile_json(char* buf, int64_t len) {
                   r.cells, r.ms);
     s += tmp;
   }
+  s += "],\"by_j\":[";
+  {
+    bool first = true;
+    for (const auto& kv : g_byj) {
+      std::snprintf(tmp, sizeof(tmp), "%s[\"%s\",%d,%lld,%lld,%.4f,%.6e]", first ? "" : ",",
+                    kKernelName[kv.first.first], kv.first.second, (long long)kv.second.launches,
+                    (long long)kv.second.cells, kv.second.ms, kv.second.flops);
+      s += tmp;
+      first = false;
+    }
+  }
   s += "],\"rounds_log\":[";
   for (size_t q = 0; q < g_rounds.size(); ++q) {
     const RoundRec& r = g_rounds[q];
@@ -1526,6 +1554,7 @@ void oi_profile_reset(void) {
   for (auto& k : g_prof) k = KStat();
   g_run = RunStat();
   g_rounds.clear();
+  g_byj.clear();
   g_ext.clear();
 }
 

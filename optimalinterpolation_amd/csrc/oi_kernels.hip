@@ -1809,7 +1809,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
     }
     fwd_update<GEMM_THREADS>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) {
-      emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1
+      if (j > 0) emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1 (empty at j = 0)
       return;
     }
     // i = j+1: add the fresh L_j+1,j L_j+1,j^T (staged in lds as X[q*XLD + m] =
@@ -2016,13 +2016,16 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
       gemm4_kmajor<false>(acc, lds, 4 * j, 0u, fpair);
     __syncthreads();  // the GEMM's last LDS reads are done
     // column j+1: partial updates of A_{i_r, j+1} (x = 0: the diagonal tile, whose
-    // L_{j+1,j} L_{j+1,j}^T part follows once that tile is final)
-    stage4_q1(acc, 0, lds);
-    if (two) stage4_q1(acc, 1, lds + NB * XLD);
-    __syncthreads();
-    emit_copy(lds, tileL(c, i1, j + 1), EMIT_SUB);
-    if (two) emit_copy(lds + NB * XLD, tileL(c, i2, j + 1), EMIT_SUB);
-    __syncthreads();
+    // L_{j+1,j} L_{j+1,j}^T part follows once that tile is final); at j = 0 the
+    // sums are empty and A - 0 is A bit for bit: no round trip through HBM
+    if (j > 0) {
+      stage4_q1(acc, 0, lds);
+      if (two) stage4_q1(acc, 1, lds + NB * XLD);
+      __syncthreads();
+      emit_copy(lds, tileL(c, i1, j + 1), EMIT_SUB);
+      if (two) emit_copy(lds + NB * XLD, tileL(c, i2, j + 1), EMIT_SUB);
+      __syncthreads();
+    }
     post_right4x2(acc, lds, Dj, two, tileL(c, i1, j), two ? tileL(c, i2, j) : nullptr, o);
     const double pre1 = fwd_preload(c, i1, j);
     const double pre2 = two ? fwd_preload(c, i2, j) : 0.0;
