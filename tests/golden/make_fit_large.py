@@ -111,6 +111,9 @@ def main():
                     help='smallest cells first (a second generator sharing the cache works from the other end)')
     ap.add_argument('--merge', nargs='?', const='', default=None,
                     help='reuse the cells of an existing fixture (default: --out) whose sizes match')
+    ap.add_argument('--partial', action='store_true',
+                    help='write the fixture from the cells whose runs are all finished (merged or cached); '
+                         'run nothing new')
     args = ap.parse_args()
     global SIZES
     if args.sizes:
@@ -131,16 +134,20 @@ def main():
         print(f"merged {len(res) // NRUNS} cells from {merge_from}", flush=True)
     jobs = sorted([(k, r) for k in range(len(SIZES)) for r in range(NRUNS) if (k, r) not in res],
                   key=lambda j: SIZES[j[0]] if args.reverse else -SIZES[j[0]])
+    if args.partial:
+        jobs = [(k, r) for k, r in jobs if os.path.exists(os.path.join(CACHE, f'k{k}_n{SIZES[k]}_r{r}.npz'))]
     with Pool(args.jobs) as pool:
         for k, r, t8, ev, inp, out, sec in pool.imap_unordered(run, jobs):
             res[(k, r)] = (t8, ev, inp, out, sec)
             print(f"cell {k} (n={SIZES[k]}) run {r}: {ev} evals, fs {t8[0]:.10f}, {sec:.0f} s", flush=True)
-    nlz_jobs = [(k, res[(k, r)][0], res[(k, 0)][2], res[(k, 0)][3])
-                for k in range(len(SIZES)) for r in range(NRUNS)]
+    cells = [k for k in range(len(SIZES)) if all((k, r) in res for r in range(NRUNS))]
+    if len(cells) < len(SIZES):
+        print(f"partial fixture: {len(cells)} of {len(SIZES)} cells complete", flush=True)
+    nlz_jobs = [(k, res[(k, r)][0], res[(k, 0)][2], res[(k, 0)][3]) for k in cells for r in range(NRUNS)]
     with Pool(args.jobs) as pool:
         nlz_all = pool.map(nlz_job, nlz_jobs)
     inx, iny, out8, evals, nlz, secs = [], [], [], [], [], []
-    for k in range(len(SIZES)):
+    for ci, k in enumerate(cells):
         _, _, inp0, y0, _ = res[(k, 0)]
         assert len(y0) == SIZES[k]
         inx.append(inp0)
@@ -151,17 +158,18 @@ def main():
             rows.append(sec)
             row8.append(t8)
             rowe.append(ev)
-            rowf.append(nlz_all[k * NRUNS + r])     # the reference's nlZ on the original order
+            rowf.append(nlz_all[ci * NRUNS + r])    # the reference's nlZ on the original order
         out8.append(row8)
         evals.append(rowe)
         nlz.append(rowf)
         secs.append(rows)
     IX, offs = ragged(inx, 3)
     IY, _ = ragged(iny, 1)
-    xs = np.array([[cell(k)[0][0, 0], cell(k)[0][0, 1], 4.0] for k in range(len(SIZES))])
+    xs = np.array([[cell(k)[0][0, 0], cell(k)[0][0, 1], 4.0] for k in cells])
     np.savez_compressed(args.out, x=IX, y=IY, offs=offs, xs=xs,
                         mean=synthetic_mean(), out8=np.array(out8), evals=np.array(evals),
-                        nlz=np.array(nlz), sizes=np.array(SIZES), sec=np.array(secs), numpy=np.__version__,
+                        nlz=np.array(nlz), sizes=np.array([SIZES[k] for k in cells]), sec=np.array(secs),
+                        numpy=np.__version__,
                         scipy=scipy.__version__, ref=REF, lines=f'{FIRST}-{LAST}')
 
 
