@@ -384,3 +384,30 @@ def test_fold_equals_per_column(monkeypatch):
         x, y = cells.xyt[cells.offs[c]:cells.offs[c + 1]], cells.z[cells.offs[c]:cells.offs[c + 1]]
         f, g = O.neg_log_ml(h[c], x, y, mX[cells.offs[c]:cells.offs[c + 1]])
         assert abs(f1[0][c] - f) <= 1e-10 * max(1.0, abs(f)), (n, f1[0][c], f)
+
+
+def test_profile_by_j_matches_kernel_totals():
+    """The per-(kernel, block column) launch table of the profile (bench.py
+    --dump) accounts for every profiled launch: per kernel its
+    launches, HIP-event milliseconds and executed flops sum to the kernel
+    totals, and the factor-panel rows cover the block columns the cells have."""
+    sizes = [300, 700, 1300]
+    cells = synthetic.make_cells(sizes, seed=41)
+    h = np.tile(np.array([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(1e-3), 0.]), (len(sizes), 1))
+    mX = np.full(len(cells.z), cells.mean)
+    _lib.profile_reset()
+    _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, h, profile=True)
+    pj = _lib.profile_json()
+    byj = pj['by_j']
+    assert byj
+    for k, v in pj['kernels'].items():
+        rows = [r for r in byj if r[0] == k]
+        if not v['launches']:
+            assert not rows
+            continue
+        assert sum(r[2] for r in rows) == v['launches'], k
+        assert abs(sum(r[4] for r in rows) - v['total_ms']) <= 1e-3 * max(1.0, v['total_ms']), k
+        if v['flops'] > 0 and k != 'k_lauum_grad':
+            assert abs(sum(r[5] for r in rows) - v['flops']) <= 1e-6 * v['flops'], k  # printed to 7 digits
+    js = sorted(r[1] for r in byj if r[0] == 'k_diag_factor')   # one row per block column 0 .. T-1
+    assert js == list(range(len(js))) and len(js) >= 2
