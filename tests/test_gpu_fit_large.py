@@ -18,13 +18,16 @@ of the reference's own noise:
   the reference's run 0 is <= 1e-8, and the fraction of cells beyond 1e-6 is
   no larger than the fraction of the reference's own permuted runs 1-4 that
   are beyond 1e-6 of its run 0 (+ one cell of slack for 27 samples);
-* work: per 500-wide n bucket the GPU's mean SMLII evaluations per cell are
-  within 10 % of the mean over the reference's 5 runs.
+* work: per 500-wide n bucket the GPU's mean SMLII evaluations per cell lie
+  inside the range of the reference's five per-run bucket means (+-10 %), and
+  over all cells inside the range of its five per-run totals (+-5 %).
 
 The GPU's nlZ at its own fitted hypers comes from oi_nlml_grad_batch (T1-equal
 to the reference's SMLII to ~1e-13, tests/test_gpu_parity.py); the
 reference's nlZ values are the fixture's (computed by the reference's SMLII on
 the original order)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -33,10 +36,12 @@ from oracle import gp_oracle as O
 from optimalinterpolation_amd import _lib
 
 pytestmark = pytest.mark.gpu
+# OI_FIT_LARGE_FIXTURE: another fixture file under tests/golden (a partial one while generating)
+FIXTURE = os.environ.get('OI_FIT_LARGE_FIXTURE', 'fit_large.npz')
 
 
 def _fit():
-    d = load_golden('fit_large.npz')
+    d = load_golden(FIXTURE)
     x, y, offs, xs, mean = d['x'].reshape(-1, 3), d['y'], d['offs'], d['xs'], float(d['mean'])
     out, status, info = _lib.gpr_batch(x, y, offs, xs, mean, x0=np.array(O.X0_PRODUCTION), opt=True,
                                        info=True)
@@ -55,7 +60,7 @@ def fit():
 
 
 def test_fixture_covers_config5_buckets():
-    d = load_golden('fit_large.npz')
+    d = load_golden(FIXTURE)
     sizes = d['sizes']
     for lo in range(500, 5000, 500):
         hi = lo + 500 if lo < 4500 else 5001
@@ -97,16 +102,34 @@ def test_large_fits_fleet_rules():
 
 
 def test_large_fits_evaluations_per_bucket():
+    """Work: the GPU's mean SMLII evaluations per cell, per 500-wide n bucket,
+    inside the range of the reference's own five per-run bucket means widened
+    by 10 %, and over the whole fixture inside the range of its five per-run
+    totals widened by 5 %.
+    (A plain +-10 % band around the reference's mean bucket count is not a
+    rule the reference itself passes: with three cells per bucket one chaotic
+    cell moves a bucket mean by more than that -- the n = 2000 cell of the
+    fixture takes 157 .. 220 evaluations over its five runs -- so the test
+    prints how many of the reference's own runs fall outside that band.)"""
     d, out, status, info, nlz_gpu, st = fit()
     sizes, evals = d['sizes'], d['evals']
-    lines = []
+    lines, ref_out = [], 0
     for lo in range(500, 5000, 500):
         hi = lo + 500 if lo < 4500 else 5001
         m = (sizes >= lo) & (sizes < hi)
+        if not m.any():   # (a partial fixture; test_fixture_covers_config5_buckets guards the real one)
+            continue
         g = float(np.mean(info[m, 3]))
-        r = float(np.mean(evals[m]))
-        lines.append((lo, g, r, g / r))
-    print("n bucket, GPU evals/cell, reference evals/cell, ratio:",
-          [(lo, round(g, 1), round(r, 1), round(q, 3)) for lo, g, r, q in lines])
-    for lo, g, r, q in lines:
-        assert abs(q - 1) <= 0.10, (lo, g, r, lines)
+        runs = [float(np.mean(evals[m, r])) for r in range(evals.shape[1])]
+        r = float(np.mean(runs))
+        ref_out += sum(abs(x / r - 1) > 0.10 for x in runs)
+        lines.append((lo, g, r, g / r, min(runs), max(runs)))
+    print("n bucket, GPU evals/cell, reference evals/cell (mean, per-run min-max), ratio:",
+          [(lo, round(g, 1), round(r, 1), (round(a, 1), round(b, 1)), round(q, 3)) for lo, g, r, q, a, b in lines])
+    print(f"reference runs outside +-10 % of their own bucket mean: {ref_out} of {len(lines) * evals.shape[1]}")
+    for lo, g, r, q, a, b in lines:
+        assert 0.9 * a <= g <= 1.1 * b, (lo, g, r, a, b, lines)
+    tot_g, tot_runs = float(np.sum(info[:, 3])), np.sum(evals, axis=0)
+    print(f"all cells: GPU {tot_g:.0f} evaluations, reference runs {tot_runs.tolist()} "
+          f"(ratio to their mean {tot_g / np.mean(tot_runs):.3f})")
+    assert 0.95 * tot_runs.min() <= tot_g <= 1.05 * tot_runs.max(), (tot_g, tot_runs)
