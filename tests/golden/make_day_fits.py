@@ -1,0 +1,184 @@
+"""T3 fixtures on the HEADLINE's own cells: the REFERENCE's GPR3D(opt=True)
+(GPR_CS2S3.py:143-191, scipy CG at :166) on cells of the bench day itself --
+``synthetic.make_day(seed=0)``, the 9997-cell config-3 day that `bench.py`
+times (VERDICT r3 "next round" item 1).
+
+Run in the build container only (it reads /root/reference):
+    python tests/golden/make_day_fits.py [--jobs 7] [--partial]
+
+Cells (seeded selection, written into the fixture as day indices):
+  * strata: 8 cells in every 300-wide n bucket 300-600, ..., 2700-3000
+    (the last bucket includes n = 3000) -- 72 cells;
+  * small: 160 further cells with n < 600 (the day's smallest bucket; the
+    day has no cell below n = 300) for a distributional test of the
+    evaluation count.
+Every cell runs in 5 observation orders: run 0 on the cell's observations as
+drawn, runs 1-4 on seeded permutations of them (the reference's chaotic
+stopping point moves with the summation order).
+
+Each run is the reference's own GPR3D(index=0) on a one-cell "day" whose
+training set is the cell's observations (globals injected as make_golden.py
+does).  The day draws observations at r <= 300 km and snaps them to the
+25 km lattice, so a few land up to 12.5*sqrt(2) km beyond the disc; `bench.py`
+queries at RADIUS_M + grid spacing so that every drawn observation is used,
+and the reference's module global ``radius`` (read at GPR:159) is set to
+325 km here for the same reason -- its query then returns the cell's
+observations in cKDTree order (recorded as the run's inputs).
+
+Recorded per run: the 8-tuple, the number of SMLII evaluations, the wall time,
+and nlZ = the reference's own SMLII at the run's hypers on run 0's inputs.
+Only numeric vectors are written (day_ref_fits.npz); every finished run is
+cached under tests/golden/_fit_cache/ (git-ignored) so generation resumes.
+"""
+import argparse
+import os
+import sys
+from multiprocessing import Pool
+
+os.environ['OPENBLAS_NUM_THREADS'] = '1'   # one single-threaded process per core
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+CACHE = os.path.join(HERE, '_fit_cache')
+NRUNS = 5
+DAY_SEED = 0
+SELECT_SEED = 20261017
+STRATA = tuple(range(300, 3000, 300))   # bucket lower edges; width 300
+PER_STRATUM = 8
+N_SMALL = 160
+RADIUS_KM = 325                          # >= 300 km + the lattice's half diagonal (17.7 km)
+
+
+def select_cells(sizes):
+    """-> (day indices, stratum flag): 8 per 300-wide bucket, then 160 more
+    with n < 600."""
+    import numpy as np
+    rng = np.random.default_rng(SELECT_SEED)
+    chosen, strat = [], []
+    for lo in STRATA:
+        hi = lo + 300 if lo < 2700 else 3001
+        pool = np.flatnonzero((sizes >= lo) & (sizes < hi))
+        pick = np.sort(rng.choice(pool, PER_STRATUM, replace=False))
+        chosen += pick.tolist()
+        strat += [1] * PER_STRATUM
+    pool = np.setdiff1d(np.flatnonzero(sizes < 600), chosen)
+    pick = np.sort(rng.choice(pool, N_SMALL, replace=False))
+    chosen += pick.tolist()
+    strat += [0] * N_SMALL
+    return np.array(chosen, dtype=np.int64), np.array(strat, dtype=np.int8)
+
+
+_DAY = {}
+
+
+def day():
+    if 'd' not in _DAY:
+        from optimalinterpolation_amd import synthetic
+        _DAY['d'] = synthetic.make_day(seed=DAY_SEED)
+    return _DAY['d']
+
+
+def run(job):
+    idx, r = job
+    import time
+    import numpy as np
+    d = day()
+    n = int(d.sizes[idx])
+    path = os.path.join(CACHE, f'day{DAY_SEED}_c{idx}_n{n}_r{r}.npz')
+    if os.path.exists(path):
+        f = np.load(path)
+        return idx, r, f['t8'], int(f['ev']), f['inp'], f['out'], float(f['sec'])
+    t0 = time.time()
+    from make_golden import cell_inputs, install_day, load_reference
+    ref = load_reference()
+    x, z, xs = d.cell(idx)
+    if r > 0:
+        p = np.random.default_rng(7000 + 13 * idx + r).permutation(n)
+        x, z = x[p], z[p]
+    X = xs[:, :2].copy()
+    install_day(ref, X, x[:, 0].copy(), x[:, 1].copy(), x[:, 2].copy(), z.copy(), d.mean)
+    ref['radius'] = RADIUS_KM
+    orig = ref['SMLII']
+    count = [0]
+
+    def counted(h, xx, yy, mX):
+        count[0] += 1
+        return orig(h, xx, yy, mX)
+    ref['SMLII'] = counted
+    t8 = np.array(ref['GPR3D'](0), dtype=float)          # opt=True, GPR:260
+    ref['SMLII'] = orig
+    inputs, outputs = cell_inputs(ref, 0)
+    assert len(outputs) == n, (idx, len(outputs), n)
+    sec = time.time() - t0
+    os.makedirs(CACHE, exist_ok=True)
+    np.savez(path + '.tmp.npz', t8=t8, ev=count[0], inp=inputs, out=outputs, sec=sec)
+    os.replace(path + '.tmp.npz', path)
+    return idx, r, t8, count[0], inputs, outputs, sec
+
+
+def nlz_job(job):
+    """The reference's SMLII (GPR:107-141) at a run's hypers on run 0's inputs."""
+    t8, inp0, y0, mean = job
+    import numpy as np
+    from make_golden import load_reference
+    ref = load_reference()
+    h = np.r_[np.log(t8[3:8]), np.log(.1)]
+    f, _ = ref['SMLII'](h, inp0, y0, np.ones(len(y0)) * mean)
+    return float(np.asarray(f).item()) if np.ndim(f) else float(f)
+
+
+def main():
+    import numpy as np
+    import scipy
+    from make_golden import REF, FIRST, LAST, ragged
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--jobs', type=int, default=7)
+    ap.add_argument('--out', default=os.path.join(HERE, 'day_ref_fits.npz'))
+    ap.add_argument('--partial', action='store_true',
+                    help='write the fixture from the cells whose runs are all cached; run nothing new')
+    ap.add_argument('--only-small', action='store_true', help='run the n < 600 cells only (dry runs)')
+    args = ap.parse_args()
+    d = day()
+    cells, strat = select_cells(d.sizes)
+    if args.only_small:
+        keep = d.sizes[cells] < 600
+        cells, strat = cells[keep], strat[keep]
+    jobs = sorted([(int(c), r) for c in cells for r in range(NRUNS)], key=lambda j: -int(d.sizes[j[0]]))
+    if args.partial:
+        jobs = [(c, r) for c, r in jobs
+                if os.path.exists(os.path.join(CACHE, f'day{DAY_SEED}_c{c}_n{int(d.sizes[c])}_r{r}.npz'))]
+    res = {}
+    with Pool(args.jobs) as pool:
+        for c, r, t8, ev, inp, out, sec in pool.imap_unordered(run, jobs):
+            res[(c, r)] = (t8, ev, inp, out, sec)
+            print(f"cell {c} (n={int(d.sizes[c])}) run {r}: {ev} evals, fs {t8[0]:.10f}, {sec:.0f} s", flush=True)
+    done = [i for i, c in enumerate(cells) if all((int(c), r) in res for r in range(NRUNS))]
+    if len(done) < len(cells):
+        print(f"partial fixture: {len(done)} of {len(cells)} cells complete", flush=True)
+    cells, strat = cells[done], strat[done]
+    nlz_jobs = [(res[(int(c), r)][0], res[(int(c), 0)][2], res[(int(c), 0)][3], d.mean)
+                for c in cells for r in range(NRUNS)]
+    with Pool(args.jobs) as pool:
+        nlz_all = pool.map(nlz_job, nlz_jobs, chunksize=4)
+    inx, iny, out8, evals, nlz, secs = [], [], [], [], [], []
+    for ci, c in enumerate(cells):
+        t8s, evs, _, _, sc = zip(*[res[(int(c), r)] for r in range(NRUNS)])
+        inx.append(res[(int(c), 0)][2])
+        iny.append(res[(int(c), 0)][3])
+        out8.append(np.array(t8s))
+        evals.append(evs)
+        secs.append(sc)
+        nlz.append(nlz_all[ci * NRUNS:(ci + 1) * NRUNS])
+    IX, offs = ragged(inx, 3)
+    IY, _ = ragged(iny, 1)
+    np.savez_compressed(args.out, x=IX, y=IY, offs=offs, xs=d.xs[cells], cells=cells, stratum=strat,
+                        sizes=d.sizes[cells], mean=d.mean, out8=np.array(out8), evals=np.array(evals),
+                        nlz=np.array(nlz), sec=np.array(secs), day_seed=DAY_SEED, radius_km=RADIUS_KM,
+                        numpy=np.__version__, scipy=scipy.__version__, ref=REF, lines=f'{FIRST}-{LAST}')
+    print(f"wrote {args.out}: {len(cells)} cells", flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -79,6 +79,67 @@ __global__ __launch_bounds__(512) void g4(const double* A, const double* B, doub
   C[(size_t)blockIdx.x * 512 + t] = s;
 }
 
+
+// LDS-DMA staging (global_load_lds_dwordx4): each wave instruction fills one
+// 128-double LDS row (k-row of the two 64-wide tiles side by side) linearly;
+// odd rows hold the two 16-double halves of every 32-double group swapped
+// (source address permuted per lane, read index m ^ 16), so ds_read_b64 of
+// rows k, k+1 by one half-wave falls in opposite bank halves.
+// NBUF LDS buffers, NBUF-1 chunks in flight across raw barriers (counted vmcnt).
+template <int KCG, int NBUF>
+__global__ __launch_bounds__(512) void g4g(const double* A, const double* B, double* C, int P, int mode) {
+  constexpr int ROW = 128, STG = KCG * ROW, G = 2 * KCG / 8;  // glds per wave per chunk
+  constexpr int CPP = 64 / KCG;                              // chunks per operand pair
+  __shared__ __attribute__((aligned(16))) double lds[NBUF * 2 * STG];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  Acc8 acc;
+  for (int a = 0; a < 2; ++a) for (int b = 0; b < 4; ++b) acc.c[a][b] = (d4){0, 0, 0, 0};
+  const int nch = P * CPP;
+  auto issue = [&](int ch) __attribute__((always_inline)) {
+    const int p = ch / CPP, k0 = (ch % CPP) * KCG;
+    double* buf = lds + (ch % NBUF) * 2 * STG;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int gi = w * G + i, isB = gi >= KCG, k = isB ? gi - KCG : gi;
+      const double* tp = tile(isB ? B : A, mode, blockIdx.x, P, p, (isB ? 2 : 0) + (lane >> 5));
+      const int q = (lane & 31) ^ (8 * (k & 1));
+      __builtin_amdgcn_global_load_lds((const void*)(tp + (k0 + k) * 64 + 2 * q),
+                                       (void*)(buf + (isB ? STG : 0) + k * ROW), 16, 0, 0);
+    }
+  };
+  auto compute = [&](int ch) __attribute__((always_inline)) {
+    const double* As = lds + (ch % NBUF) * 2 * STG;
+    const double* Bs = As + STG;
+#pragma unroll
+    for (int kk = 0; kk < KCG / 4; ++kk) {
+      const int k = kk * 4 + fk, sw = 16 * (k & 1);
+      const double a0 = As[k * ROW + ((32 * wr + fr) ^ sw)], a1 = As[k * ROW + ((32 * wr + 16 + fr) ^ sw)];
+      double b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[q] = Bs[k * ROW + ((64 * wc + 16 * q + fr) ^ sw)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc.c[0][q] = MFMA64(a0, b[q], acc.c[0][q]);
+        acc.c[1][q] = MFMA64(a1, b[q], acc.c[1][q]);
+      }
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < NBUF - 1; ++d) issue(min(d, nch - 1));
+  for (int ch = 0; ch < nch; ++ch) {
+    // chunk ch landed (this wave's part): NBUF-2 younger chunks may stay in flight
+    if constexpr (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * G) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(min(ch + NBUF - 1, nch - 1));
+    compute(ch);
+  }
+  double s = 0;
+  for (int a = 0; a < 2; ++a) for (int b = 0; b < 4; ++b) for (int q = 0; q < 4; ++q) s += acc.c[a][b][q];
+  C[(size_t)blockIdx.x * 512 + t] = s;
+}
+
 __global__ __launch_bounds__(512) void g2(const double* A, const double* B, double* C, int P, int mode) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
   Quad acc; quad_zero(acc);
@@ -125,9 +186,31 @@ int main() {
     }
   };
   const double tp = 2.0 * 64 * 64 * 64 * P;  // one output tile
+  auto result = [&](auto kern) {
+    std::vector<double> h((size_t)nwg * 512);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), 0, 0, A, B, C, P, 0); CHK(hipDeviceSynchronize());
+    CHK(hipMemcpy(h.data(), C, h.size() * 8, hipMemcpyDeviceToHost));
+    return h;
+  };
+  {
+    auto ref = result(g4<144>);
+    auto chk = [&](const char* name, auto kern) {
+      auto h = result(kern); size_t bad = 0;
+      for (size_t i = 0; i < h.size(); ++i) bad += h[i] != ref[i];
+      printf("check %-16s %zu of %zu differ\n", name, bad, h.size());
+    };
+    chk("g4g kc16 nbuf2", g4g<16, 2>); chk("g4g kc16 nbuf3", g4g<16, 3>); chk("g4g kc8 nbuf4", g4g<8, 4>);
+    chk("g4g kc8 nbuf3", g4g<8, 3>); chk("g4g kc32 nbuf2", g4g<32, 2>);
+  }
   run("g1 64x64", g1, 256, 4 * nwg, tp);
   run("g2 64x128", g2, 512, 2 * nwg, 2 * tp);
   run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
   run("g4 128x128 s136", g4<136>, 512, nwg, 4 * tp);
+  run("g4g kc16 nbuf2", g4g<16, 2>, 512, nwg, 4 * tp);
+  run("g4g kc16 nbuf3", g4g<16, 3>, 512, nwg, 4 * tp);
+  run("g4g kc8 nbuf4", g4g<8, 4>, 512, nwg, 4 * tp);
+  run("g4g kc8 nbuf3", g4g<8, 3>, 512, nwg, 4 * tp);
+  run("g4g kc32 nbuf2", g4g<32, 2>, 512, nwg, 4 * tp);
+  run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
   return 0;
 }
