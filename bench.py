@@ -64,6 +64,10 @@ def parse():
     p.add_argument('--season-shares', type=int, default=8,
                    help='season workload: the 12.5 km day is LPT-split into this many GPU shares; rank r '
                         'fits share r (config 5 = 8 shares on 8 GPUs; at N = 1 one 1/8 share)')
+    p.add_argument('--day-shares', type=int, default=0,
+                   help='day workload: LPT-split the day into this many GPU shares (default: one per rank) and fit '
+                        'share --share (default: this rank\'s) -- e.g. one 8-GPU share of config 4 on one GPU')
+    p.add_argument('--share', type=int, default=-1, help='day workload with --day-shares: the share to fit')
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--slices', default='ordered', choices=['lpt', 'ordered'],
                    help='day slices: equal-cost LPT mixes (lpt) or consecutive runs of the '
@@ -209,16 +213,25 @@ def build_slices(args, rank, world):
                   "x0": "GPR_CS2S3.py:217", "slices": args.slices}
         day_sites = driver.site_counts(day)
         if args.workload == 'day':
-            parts = driver.lpt_partition(driver.cell_costs(day.sizes, sites=day_sites), world)
-            mine = day.subset(parts[rank])
-            mine_sites = day_sites[parts[rank]]
-            cfg = {"workload": ("25km pan-Arctic day, opt=True fit+predict per cell "
-                                f"(config {'3' if world == 1 else '4'}: the whole day on {world} GPU"
-                                f"{'s' if world > 1 else ''}, one slice per step)"),
-                   **common, "cells_total": int(day.ncell), "cells_per_rank": int(mine.ncell),
-                   "parallelism": f"dp{world} (LPT cell partition on E(n) m^3, one RCCL gather)"}
+            shares = max(int(args.day_shares), world)
+            parts = driver.lpt_partition(driver.cell_costs(day.sizes, sites=day_sites), shares)
+            idx = [args.share if (args.share >= 0 and world == 1) else r for r in range(world)]
+            mine = day.subset(parts[idx[rank]])
+            mine_sites = day_sites[parts[idx[rank]]]
+            if shares == world:
+                cfg = {"workload": ("25km pan-Arctic day, opt=True fit+predict per cell "
+                                    f"(config {'3' if world == 1 else '4'}: the whole day on {world} GPU"
+                                    f"{'s' if world > 1 else ''}, one slice per step)"),
+                       **common, "cells_total": int(day.ncell), "cells_per_rank": int(mine.ncell),
+                       "parallelism": f"dp{world} (LPT cell partition on E(n) m^3, one RCCL gather)"}
+            else:
+                cfg = {"workload": (f"config 4 share: the 25km day LPT-split into {shares} GPU shares, this run "
+                                    f"fits share(s) {idx} ({world} GPU), one slice per step"),
+                       **common, "cells_total": int(day.ncell), "cells_per_rank": int(mine.ncell),
+                       "shares": shares, "share": idx[rank],
+                       "parallelism": f"{shares}-way LPT partition on E(n) m^3; {world} of them here"}
             scaling = "strong"
-            counts_all = [len(p) for p in parts]
+            counts_all = [len(parts[i]) for i in idx]
         else:
             mine, mine_sites = day, day_sites
             cfg = {"workload": "one synthetic 25km day per rank (seed + rank), opt=True fit+predict, "

@@ -1,0 +1,855 @@
+// Hand-written batched dense fp64 linear algebra for the Nystrom variant
+// (GP_example.ipynb, "NB1": Nystroem's np.linalg.eigh(Kmm), SMLII's
+// np.linalg.cholesky and the n x M matrix products) on gfx950 -- no LAPACK,
+// rocSOLVER or rocBLAS.  Interface: oi_linalg.h.
+//
+//   k_gemm        C = alpha op(A) op(B) + beta C, 64 x 64 output tile per
+//                 256-thread workgroup on v_mfma_f64_16x16x4f64 (the oi_gemm.h
+//                 quadrant layout), operands staged global -> registers -> LDS
+//                 in 16-deep chunks, results staged through LDS for coalesced
+//                 column stores; one launch covers a batch of differently
+//                 sized products (grid.y = product)
+//   k_gemv        y = alpha op(A) x + beta y
+//   k_potrf_tile  Cholesky + inverse of one 64 x 64 diagonal block per matrix
+//                 (the blocked right-looking factorisation: potrf_tile ->
+//                 panel product with the block inverse -> lower-tile update)
+//   k_sytrd       Householder tridiagonalisation (LAPACK dsytrd / dlatrd,
+//                 lower) of one matrix per 512-thread workgroup: per column
+//                 the symmetric product over the trailing lower triangle (each
+//                 wave owns columns; the transposed half is accumulated in
+//                 per-wave LDS vectors, summed in fixed order), panel
+//                 corrections, then the rank-2*32 trailing update per panel on
+//                 the MFMA core; V (unit lower, clean copy) and T (dlarft,
+//                 forward columnwise) kept per 32-column panel
+//   k_stebz_stein eigenvalues of the tridiagonal by bisection on Sturm counts
+//                 (dstebz), eigenvectors by inverse iteration with partial
+//                 pivoting (dlagtf / dlagts; dstein), one thread per
+//                 eigenvalue, pseudo-random start per eigenvalue
+//   k_mgs_panel   classical Gram-Schmidt twice inside a 32-vector panel, a
+//                 fresh start vector where one collapses (repeated
+//                 eigenvalues); between panels block Gram-Schmidt twice
+//                 (BCGS2) on k_gemm
+//   back-transform U = Q Z, one block reflector I - V T V' per panel (k_gemm)
+// The algorithm is modelled step for step in tools/eigh_model.py.
+//
+// Reductions run in a fixed order, so a matrix's results do not depend on the
+// batch it is in.
+#include "oi_linalg.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "oi_gemm.h"
+
+namespace oila {
+
+#define LC(expr)                                                                                \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) throw LinalgErr{std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+// ------------------------------------------------------------------ k_gemm
+#define GT 64
+#define GKC 16
+#define GLD 80  // LDS row stride of a staged 16 x 64 chunk (rows k, k+1 in opposite bank halves)
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GKC * GLD];
+  const Gemm g = gs[blockIdx.y];
+  const int tm = (g.m + GT - 1) / GT, tn = (g.n + GT - 1) / GT;
+  if ((int)blockIdx.x >= tm * tn) return;
+  const int it = blockIdx.x % tm, jt = blockIdx.x / tm;
+  if (g.tri == 1 && it < jt) return;
+  int kmax = g.k;
+  if (g.tri == 2) kmax = min(kmax, GT * (jt + 1));
+  const int m0 = GT * it, n0 = GT * jt;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  Quad acc;
+  quad_zero(acc);
+  const int nch = (kmax + GKC - 1) / GKC;
+  double ra[4], rb[4];
+  // element e = t + 256 q of a 64 x 16 chunk: A(m, k) and op(B)(k, n)
+  auto load = [&](int ch) __attribute__((always_inline)) {
+    const int k0 = ch * GKC;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 256 * q;
+      int m, k;
+      if (TA) { k = e & 15; m = e >> 4; } else { m = e & 63; k = e >> 6; }
+      const int gm = m0 + m, gk = k0 + k;
+      ra[q] = (gm < g.m && gk < kmax) ? (TA ? g.A[gk + (size_t)g.lda * gm] : g.A[gm + (size_t)g.lda * gk]) : 0.0;
+      int n, kb;
+      if (TB) { n = e & 63; kb = e >> 6; } else { kb = e & 15; n = e >> 4; }
+      const int gn = n0 + n, gkb = k0 + kb;
+      rb[q] = (gn < g.n && gkb < kmax) ? (TB ? g.B[gn + (size_t)g.ldb * gkb] : g.B[gkb + (size_t)g.ldb * gn]) : 0.0;
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    double* As = lds + buf * 2 * GKC * GLD;
+    double* Bs = As + GKC * GLD;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 256 * q;
+      if (TA) As[(e & 15) * GLD + (e >> 4)] = ra[q]; else As[(e >> 6) * GLD + (e & 63)] = ra[q];
+      if (TB) Bs[(e >> 6) * GLD + (e & 63)] = rb[q]; else Bs[(e & 15) * GLD + (e >> 4)] = rb[q];
+    }
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const double* As = lds + buf * 2 * GKC * GLD;
+    const double* Bs = As + GKC * GLD;
+#pragma unroll
+    for (int kk = 0; kk < GKC / 4; ++kk) {
+      const int k = kk * 4 + fk;
+      const double a0 = As[k * GLD + 32 * wr + fr], a1 = As[k * GLD + 32 * wr + 16 + fr];
+      const double b0 = Bs[k * GLD + 32 * wc + fr], b1 = Bs[k * GLD + 32 * wc + 16 + fr];
+      acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+      acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+      acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+      acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+    }
+  };
+  if (nch > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      if (ch + 1 < nch) load(ch + 1);
+      compute(ch & 1);
+      if (ch + 1 < nch) store((ch + 1) & 1);
+      __syncthreads();
+    }
+  }
+  // stage the tile column-major in LDS (X[n * 65 + m]) for coalesced stores
+  double* X = lds;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) X[acc1_col(nb) * 65 + acc1_row(mb, r)] = acc.c[mb][nb][r];
+  __syncthreads();
+  for (int e = t; e < GT * GT; e += 256) {
+    const int m = e & 63, n = e >> 6, gm = m0 + m, gn = n0 + n;
+    if (gm >= g.m || gn >= g.n) continue;
+    double* c = g.C + gm + (size_t)g.ldc * gn;
+    const double v = g.alpha * X[n * 65 + m];
+    *c = g.beta == 0.0 ? v : v + g.beta * *c;
+  }
+}
+
+// ------------------------------------------------------------------ k_gemv
+// trans: y_j = alpha sum_i A(i, j) x_i + beta y_j, one wave per output;
+// else  y_i = alpha sum_j A(i, j) x_j + beta y_i, one thread per output.
+template <bool TRANS>
+__global__ __launch_bounds__(256) void k_gemv(const Gemv* __restrict__ gs) {
+  const Gemv g = gs[blockIdx.y];
+  if (TRANS) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= g.n) return;
+    const double* a = g.A + (size_t)g.lda * j;
+    double s = 0.0;
+    for (int i = lane; i < g.m; i += 64) s += a[i] * g.x[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (lane == 0) g.y[j] = g.beta == 0.0 ? g.alpha * s : g.alpha * s + g.beta * g.y[j];
+  } else {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= g.m) return;
+    double s = 0.0;
+    for (int j = 0; j < g.n; ++j) s += g.A[i + (size_t)g.lda * j] * g.x[j];
+    g.y[i] = g.beta == 0.0 ? g.alpha * s : g.alpha * s + g.beta * g.y[i];
+  }
+}
+
+// ------------------------------------------------------------ k_potrf_tile
+// Block jb of a blocked right-looking Cholesky: factor the (updated) diagonal
+// block A(jb:jb+nb, jb:jb+nb) in place (lower, nb = min(64, M - jb)) and write
+// its inverse to dinv[jb/64] (64 x 64, column-major, identity beyond nb).
+// Pivot <= 0 or NaN -> info = 1 (LAPACK dpotrf's info > 0; NB1's LinAlgError).
+// One 64-thread wave per matrix, the block in LDS (row r = lane).
+__global__ __launch_bounds__(64) void k_potrf_tile(const Chol* __restrict__ cs, int jb) {
+  __shared__ double L[64 * 65];
+  const Chol c = cs[blockIdx.x];
+  if (jb >= c.M) return;
+  const int nb = min(64, c.M - jb), r = threadIdx.x;
+  double* A = c.A + jb + (size_t)c.lda * jb;
+  for (int j = 0; j < 64; ++j)
+    L[r * 65 + j] = (r < nb && j < nb) ? (j <= r ? A[r + (size_t)c.lda * j] : 0.0) : (r == j ? 1.0 : 0.0);
+  __syncthreads();
+  bool bad = false;
+  for (int j = 0; j < nb; ++j) {
+    const double p = L[j * 65 + j];
+    if (!(p > 0.0)) bad = true;
+    const double ljj = sqrt(p);
+    __syncthreads();
+    if (r == j) L[j * 65 + j] = ljj;
+    if (r > j) L[r * 65 + j] = L[r * 65 + j] / ljj;
+    __syncthreads();
+    if (r > j) {
+      const double lrj = L[r * 65 + j];
+      for (int k = j + 1; k <= r; ++k) L[r * 65 + k] -= lrj * L[k * 65 + j];
+    }
+    __syncthreads();
+  }
+  if (bad && r == 0) *c.info = 1;
+  // inverse: lane j forms column j of L^-1 by forward substitution
+  double* D = c.dinv + (size_t)(jb / 64) * 4096;
+  {
+    const int j = r;
+    double x[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) x[i] = 0.0;
+    // x_i = (delta_ij - sum_{k<i} L_ik x_k) / L_ii, i >= j
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      if (i < j) continue;
+      double s = i == j ? 1.0 : 0.0;
+      for (int k = j; k < i; ++k) s -= L[i * 65 + k] * x[k];
+      x[i] = s / L[i * 65 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) D[i + 64 * j] = x[i];
+  }
+  __syncthreads();
+  for (int j = 0; j < nb; ++j)
+    if (r >= j && r < nb) A[r + (size_t)c.lda * j] = L[r * 65 + j];
+}
+
+// ------------------------------------------------------------------ k_sytrd
+#define TNB 32   // panel width
+#define SY_T 512 // threads
+#define SY_W (SY_T / 64)
+
+struct EighWs {  // per-matrix workspace carve-up (eigh_workspace_doubles)
+  double *Vc, *Ws, *T, *d, *e, *tau, *scr, *H, *X, *Y;
+};
+__host__ __device__ inline EighWs carve(double* w, int M) {
+  EighWs s;
+  const size_t MM = (size_t)M * M;
+  s.Vc = w;
+  s.scr = s.Vc + MM;               // 6 M^2: stein's LU factors and iterate
+  s.Ws = s.scr + 6 * MM;           // M x 32
+  s.H = s.Ws + (size_t)M * TNB;    // M x 32
+  s.X = s.H + (size_t)M * TNB;     // 32 x M
+  s.Y = s.X + (size_t)M * TNB;     // 32 x M
+  s.T = s.Y + (size_t)M * TNB;     // panels x 32 x 32
+  s.d = s.T + ((size_t)(M + TNB - 1) / TNB + 1) * TNB * TNB;
+  s.e = s.d + M + 1;
+  s.tau = s.e + M + 1;
+  return s;
+}
+size_t eigh_workspace_doubles(int M) {
+  const size_t MM = (size_t)M * M;
+  return 7 * MM + 4 * (size_t)M * TNB + ((size_t)(M + TNB - 1) / TNB + 1) * TNB * TNB + 3 * (size_t)M + 16;
+}
+
+template <int NV>
+__device__ __forceinline__ void wg_sum(double (&v)[NV], double* red) {
+  // fixed-order block reduction over SY_T threads; every thread gets the sums
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_down(v[q], o, 64);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[w * NV + q] = v[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double s = red[q];
+    for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) s += red[ww * NV + q];
+    v[q] = s;
+  }
+  __syncthreads();
+}
+
+// dynamic LDS: yw[SY_W][M] | v[M] | y[M] | red[64] | pan[2 * TNB] | G[TNB * TNB]
+__global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
+  extern __shared__ double sm[];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double* A = E.A;
+  EighWs ws = carve(E.work, M);
+  double* yw = sm;
+  double* v = yw + (size_t)SY_W * M;
+  double* y = v + M;
+  double* red = y + M;
+  double* pan = red + 64;  // pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v
+  double* G = pan + 2 * TNB; // TNB x TNB Gram of a panel's V (dlarft)
+  for (int i = t; i < SY_W * M; i += SY_T) yw[i] = 0.0;
+  if (M == 1 && t == 0) ws.d[0] = A[0];
+  __syncthreads();
+  for (int p = 0; p < M - 1; p += TNB) {
+    const int nb = min(TNB, M - 1 - p);
+    for (int i = 0; i < nb; ++i) {
+      const int g = p + i;
+      // (1) column g with the panel's previous columns: A(r,g) -= V(r,q) W(g,q) + W(r,q) V(g,q)
+      if (i > 0) {
+        for (int r = g + t; r < M; r += SY_T) {
+          double s = A[r + (size_t)ld * g];
+          for (int q = 0; q < i; ++q) {
+            const double* vq = ws.Vc + (size_t)M * (p + q);
+            const double* wq = ws.Ws + (size_t)M * q;
+            s -= vq[r] * wq[g] + wq[r] * vq[g];
+          }
+          A[r + (size_t)ld * g] = s;
+        }
+        __syncthreads();
+      }
+      // (2) reflector annihilating A(g+2:M, g) (dlarfg)
+      double xs[1] = {0.0};
+      for (int r = g + 2 + t; r < M; r += SY_T) {
+        const double a = A[r + (size_t)ld * g];
+        xs[0] += a * a;
+      }
+      wg_sum<1>(xs, red);
+      const double alpha = A[g + 1 + (size_t)ld * g];
+      const double xn = sqrt(xs[0]);
+      double tau, beta, scal;
+      if (xn == 0.0) {
+        tau = 0.0;
+        beta = alpha;
+        scal = 0.0;
+      } else {
+        beta = -copysign(sqrt(alpha * alpha + xn * xn), alpha);
+        tau = (beta - alpha) / beta;
+        scal = 1.0 / (alpha - beta);
+      }
+      double* vg = ws.Vc + (size_t)M * g;
+      for (int r = t; r < M; r += SY_T) {
+        const double x = r < g + 1 ? 0.0 : r == g + 1 ? 1.0 : A[r + (size_t)ld * g] * scal;
+        v[r] = x;
+        vg[r] = x;
+      }
+      if (t == 0) {
+        ws.d[g] = A[g + (size_t)ld * g];
+        ws.e[g] = beta;
+        ws.tau[g] = tau;
+      }
+      __syncthreads();
+      // (3) y = A22 v over the lower triangle of A(g+1:M, g+1:M): wave wv owns
+      // columns c = g+1+wv, +SY_W, ...; the transposed half goes to yw[wv][r]
+      double* myw = yw + (size_t)wv * M;
+      for (int c = g + 1 + wv; c < M; c += SY_W) {
+        const double* col = A + (size_t)ld * c;
+        const double vc = v[c];
+        double dot = 0.0;
+        for (int r = c + lane; r < M; r += 64) {
+          const double a = col[r];
+          dot += a * v[r];
+          if (r > c) myw[r] += a * vc;
+        }
+        for (int o = 32; o > 0; o >>= 1) dot += __shfl_down(dot, o, 64);
+        if (lane == 0) myw[c] += dot;
+      }
+      // panel corrections: pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g)
+      for (int jq = wv; jq < 2 * i; jq += SY_W) {
+        const int q = jq % i;
+        const double* col = jq < i ? ws.Ws + (size_t)M * q : ws.Vc + (size_t)M * (p + q);
+        double s = 0.0;
+        for (int r = g + 1 + lane; r < M; r += 64) s += col[r] * v[r];
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+        if (lane == 0) pan[(jq < i ? 0 : TNB) + q] = s;
+      }
+      __syncthreads();
+      // (4) w = tau (y - V (W'v) - W (V'v)), then w += -tau/2 (w'v) v
+      double sv[1] = {0.0};
+      for (int r = g + 1 + t; r < M; r += SY_T) {
+        double s = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < SY_W; ++ww) {
+          s += yw[(size_t)ww * M + r];
+          yw[(size_t)ww * M + r] = 0.0;
+        }
+        for (int q = 0; q < i; ++q)
+          s -= ws.Vc[(size_t)M * (p + q) + r] * pan[q] + ws.Ws[(size_t)M * q + r] * pan[TNB + q];
+        const double wr = tau * s;
+        y[r] = wr;
+        sv[0] += wr * v[r];
+      }
+      wg_sum<1>(sv, red);
+      const double a2 = -0.5 * tau * sv[0];
+      double* wcol = ws.Ws + (size_t)M * i;
+      for (int r = t; r < M; r += SY_T) wcol[r] = r <= g ? 0.0 : y[r] + a2 * v[r];
+      __syncthreads();
+    }
+    // T of the block reflector H_p ... H_{p+nb-1} = I - V T V' (dlarft, forward
+    // columnwise): T(i,i) = tau_i, T(0:i, i) = -tau_i T(0:i, 0:i) (V(:, 0:i)' v_i)
+    double* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
+    for (int jq = wv; jq < nb * nb; jq += SY_W) {
+      const int a = jq % nb, b = jq / nb;
+      if (a >= b) continue;
+      const double* va = ws.Vc + (size_t)M * (p + a);
+      const double* vb = ws.Vc + (size_t)M * (p + b);
+      double s = 0.0;
+      for (int r = p + b + 1 + lane; r < M; r += 64) s += va[r] * vb[r];
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+      if (lane == 0) G[a * TNB + b] = s;
+    }
+    __syncthreads();
+    if (t == 0) {
+      for (int b = 0; b < TNB; ++b)
+        for (int a = 0; a < TNB; ++a) Tp[a + TNB * b] = 0.0;
+      for (int b = 0; b < nb; ++b) {
+        const double tb = ws.tau[p + b];
+        Tp[b + TNB * b] = tb;
+        for (int a = 0; a < b; ++a) {
+          double s = 0.0;
+          for (int k = a; k < b; ++k) s += Tp[a + TNB * k] * G[k * TNB + b];
+          Tp[a + TNB * b] = -tb * s;
+        }
+      }
+    }
+    __syncthreads();
+    // trailing update A(q0:M, q0:M) -= V W' + W V' (lower triangle), 32 x 32
+    // quadrants of the MFMA core, operands [V | W] (rows) x [W | V] (columns)
+    const int q0 = p + nb, L = M - q0;
+    if (L > 0) {
+      const int nq = (L + 31) / 32;
+      const int fr = lane & 15, fk = lane >> 4;
+      for (int task = wv; task < nq * nq; task += SY_W) {
+        const int bi = task % nq, bj = task / nq;
+        if (bi < bj) continue;
+        const int r0 = q0 + 32 * bi, c0 = q0 + 32 * bj;
+        Quad acc;
+        quad_zero(acc);
+        for (int kk = 0; kk < 2 * TNB / 4; ++kk) {
+          const int k = 4 * kk + fk, q = k % TNB;
+          const bool first = k < TNB;  // k < 32: V(r) W(c)', else W(r) V(c)'
+          const double* Ar = first ? ws.Vc + (size_t)M * (p + q) : ws.Ws + (size_t)M * q;
+          const double* Bc = first ? ws.Ws + (size_t)M * q : ws.Vc + (size_t)M * (p + q);
+          const bool live = q < nb;
+          double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+          if (live) {
+            const int ra = r0 + fr, rb = r0 + 16 + fr, ca = c0 + fr, cb = c0 + 16 + fr;
+            a0 = ra < M ? Ar[ra] : 0.0;
+            a1 = rb < M ? Ar[rb] : 0.0;
+            b0 = ca < M ? Bc[ca] : 0.0;
+            b1 = cb < M ? Bc[cb] : 0.0;
+          }
+          acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
+          acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
+          acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
+          acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int nbk = 0; nbk < 2; ++nbk)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int r = r0 + 16 * mb + (lane >> 4) + 4 * rr, c = c0 + 16 * nbk + (lane & 15);
+              if (r < M && c < M && r >= c) A[r + (size_t)ld * c] -= acc.c[mb][nbk][rr];
+            }
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0 && M > 1) ws.d[M - 1] = A[(M - 1) + (size_t)ld * (M - 1)];
+}
+
+// ------------------------------------------------------------ k_stebz_stein
+__device__ __forceinline__ double start_value(int k, int i) {
+  // deterministic pseudo-random start (splitmix64 of (k, i)) in [-1, 1)
+  unsigned long long h = (unsigned long long)i * 0x9E3779B97F4A7C15ull + (unsigned long long)(k + 1) * 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 31;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 29;
+  return (double)(h >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+}
+
+// dynamic LDS: d[M] | e2[M] | red[64]
+__global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ es) {
+  extern __shared__ double sm[];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M, t = threadIdx.x;
+  EighWs ws = carve(E.work, M);
+  double* d = sm;
+  double* e2 = d + M;
+  double* red = e2 + M;
+  for (int i = t; i < M; i += blockDim.x) {
+    d[i] = ws.d[i];
+    e2[i] = i < M - 1 ? ws.e[i] * ws.e[i] : 0.0;
+  }
+  __syncthreads();
+  if (t == 0) {  // Gershgorin interval, ||T||, pivmin (dstebz)
+    double gl = d[0], gu = d[0], emax2 = 0.0;
+    for (int i = 0; i < M; ++i) {
+      const double ae = (i > 0 ? fabs(ws.e[i - 1]) : 0.0) + (i < M - 1 ? fabs(ws.e[i]) : 0.0);
+      gl = fmin(gl, d[i] - ae);
+      gu = fmax(gu, d[i] + ae);
+      emax2 = fmax(emax2, e2[i]);
+    }
+    const double tnorm = fmax(fabs(gl), fabs(gu));
+    const double eps = 2.220446049250313e-16, pivmin = 2.2250738585072014e-308 * fmax(1.0, emax2);
+    red[0] = gl - 2.1 * tnorm * eps * M - 2.1 * pivmin;
+    red[1] = gu + 2.1 * tnorm * eps * M + 2.1 * pivmin;
+    red[2] = tnorm;
+    red[3] = pivmin;
+  }
+  __syncthreads();
+  const double GL = red[0], GU = red[1], tnorm = red[2], pivmin = red[3];
+  const double eps = 2.220446049250313e-16;
+  const size_t MM = (size_t)M * M;
+  double* sa = ws.scr;          // U diagonal
+  double* sb = sa + MM;         // U first superdiagonal
+  double* sc = sb + MM;         // U second superdiagonal
+  double* sl = sc + MM;         // L multipliers
+  double* sp = sl + MM;         // row interchange flags
+  double* sx = sp + MM;         // iterate
+  for (int k = t; k < M; k += blockDim.x) {
+    // eigenvalue k (ascending): count(x) = #eigenvalues < x; lambda_k = sup{x : count(x) <= k}
+    double lo = GL, hi = GU;
+    for (int it = 0; it < 128; ++it) {
+      const double mid = 0.5 * (lo + hi);
+      if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin || mid == lo || mid == hi) break;
+      int cnt = 0;
+      double q = d[0] - mid;
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+      for (int i = 1; i < M; ++i) {
+        q = d[i] - mid - e2[i - 1] / q;
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+      }
+      if (cnt <= k) lo = mid;
+      else hi = mid;
+    }
+    const double lam = 0.5 * (lo + hi);
+    E.w[k] = lam;
+    // T - lam I = P L U (dlagtf), factors at [i * M + k]
+    {
+      double ak = d[0] - lam, bk = M > 1 ? ws.e[0] : 0.0;
+      for (int i = 0; i < M - 1; ++i) {
+        const double sub = ws.e[i];
+        const double an = d[i + 1] - lam, bn = i + 1 < M - 1 ? ws.e[i + 1] : 0.0;
+        double m, cnew = 0.0, a_i, b_i, a_next, b_next, piv = 0.0;
+        if (fabs(ak) >= fabs(sub)) {
+          m = ak != 0.0 ? sub / ak : 0.0;
+          a_i = ak;
+          b_i = bk;
+          a_next = an - m * bk;
+          b_next = bn;
+        } else {
+          m = ak / sub;
+          piv = 1.0;
+          a_i = sub;
+          b_i = an;
+          a_next = bk - m * an;
+          if (i < M - 2) {
+            cnew = bn;
+            b_next = -m * cnew;
+          } else {
+            b_next = bn;
+          }
+        }
+        const size_t o = (size_t)i * M + k;
+        sa[o] = a_i;
+        sb[o] = b_i;
+        sc[o] = cnew;
+        sl[o] = m;
+        sp[o] = piv;
+        ak = a_next;
+        bk = b_next;
+      }
+      const size_t o = (size_t)(M - 1) * M + k;
+      sa[o] = ak;
+      sb[o] = 0.0;
+      sc[o] = 0.0;
+      sl[o] = 0.0;
+      sp[o] = 0.0;
+    }
+    for (int i = 0; i < M; ++i) sx[(size_t)i * M + k] = start_value(k, i);
+    const double tol = eps * tnorm;
+    for (int iter = 0; iter < 2; ++iter) {
+      // forward: apply P and L
+      double prev = sx[k];
+      for (int i = 0; i < M - 1; ++i) {
+        const size_t o = (size_t)i * M + k;
+        const double nx = sx[o + M];
+        if (sp[o] != 0.0) {
+          sx[o] = nx;
+          prev = prev - sl[o] * nx;
+        } else {
+          sx[o] = prev;
+          prev = nx - sl[o] * prev;
+        }
+      }
+      sx[(size_t)(M - 1) * M + k] = prev;
+      // backward with U, tiny pivots perturbed (dlagts, job = -1)
+      double x1 = 0.0, x2 = 0.0, amax = 0.0;
+      for (int i = M - 1; i >= 0; --i) {
+        const size_t o = (size_t)i * M + k;
+        double s = sx[o] - sb[o] * x1 - sc[o] * x2;
+        double a = sa[o];
+        if (fabs(a) < tol) a = a >= 0.0 ? tol : -tol;
+        const double xi = s / a;
+        sx[o] = xi;
+        x2 = x1;
+        x1 = xi;
+        amax = fmax(amax, fabs(xi));
+      }
+      const double inv = 1.0 / amax;
+      for (int i = 0; i < M; ++i) sx[(size_t)i * M + k] *= inv;
+    }
+    double nrm = 0.0;
+    for (int i = 0; i < M; ++i) {
+      const double x = sx[(size_t)i * M + k];
+      nrm += x * x;
+    }
+    const double inv = 1.0 / sqrt(nrm);
+    double* z = E.A + (size_t)E.lda * k;
+    for (int i = 0; i < M; ++i) z[i] = sx[(size_t)i * M + k] * inv;
+  }
+}
+
+// ------------------------------------------------------------ k_mgs_panel
+// Columns [p, q) of Z (already orthogonal to columns < p): classical
+// Gram-Schmidt twice against the panel's earlier columns, normalise; a column
+// that collapses (repeated eigenvalue) is replaced by a fresh start vector
+// projected out of every earlier column.
+#define MG_T 256
+__global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es, int p) {
+  __shared__ double red[4 * 33];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M;
+  if (p >= M) return;
+  const int q = min(M, p + TNB), t = threadIdx.x, lane = t & 63, w = t >> 6;
+  double* Z = E.A;
+  const size_t ld = E.lda;
+  auto reduce = [&](double (&v)[33]) {  // fixed-order sums of 33 values
+#pragma unroll
+    for (int a = 0; a < 33; ++a)
+      for (int o = 32; o > 0; o >>= 1) v[a] += __shfl_down(v[a], o, 64);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+      for (int a = 0; a < 33; ++a) red[w * 33 + a] = v[a];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 33; ++a) v[a] = ((red[a] + red[33 + a]) + red[66 + a]) + red[99 + a];
+    __syncthreads();
+  };
+  for (int j = p; j < q; ++j) {
+    double* zj = Z + ld * j;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+      const int lo = attempt == 0 ? p : 0;  // a fresh vector is projected out of everything
+      double dv[33];
+#pragma unroll
+      for (int a = 0; a < 33; ++a) dv[a] = 0.0;
+      for (int i = t; i < M; i += MG_T) dv[32] += zj[i] * zj[i];
+      reduce(dv);
+      const double n0 = dv[32];
+      for (int pass = 0; pass < 2; ++pass) {
+        for (int b0 = lo; b0 < j; b0 += 32) {
+          const int nb = min(32, j - b0);
+#pragma unroll
+          for (int a = 0; a < 33; ++a) dv[a] = 0.0;
+          for (int i = t; i < M; i += MG_T) {
+            const double x = zj[i];
+#pragma unroll
+            for (int a = 0; a < 32; ++a)
+              if (a < nb) dv[a] += Z[ld * (b0 + a) + i] * x;
+          }
+          reduce(dv);
+          for (int i = t; i < M; i += MG_T) {
+            double x = zj[i];
+#pragma unroll
+            for (int a = 0; a < 32; ++a)
+              if (a < nb) x -= dv[a] * Z[ld * (b0 + a) + i];
+            zj[i] = x;
+          }
+          __syncthreads();
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 33; ++a) dv[a] = 0.0;
+      for (int i = t; i < M; i += MG_T) dv[32] += zj[i] * zj[i];
+      reduce(dv);
+      const double n1 = dv[32];
+      if (n1 > 1e-4 * n0 && n1 > 0.0) {
+        const double inv = 1.0 / sqrt(n1);
+        for (int i = t; i < M; i += MG_T) zj[i] *= inv;
+        __syncthreads();
+        break;
+      }
+      for (int i = t; i < M; i += MG_T) zj[i] = start_value(j + 7919 * (attempt + 1), i);
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------- host --
+Stager::~Stager() {
+  if (host_) (void)hipHostFree(host_);
+  if (dev_) (void)hipFree(dev_);
+  for (auto& pr : retired_) {
+    (void)hipHostFree(pr.first);
+    (void)hipFree(pr.second);
+  }
+}
+
+const void* Stager::put_bytes(const void* p, size_t bytes) {
+  const size_t need = (off_ + bytes + 255) & ~(size_t)255;
+  if (need > cap_) {
+    if (host_) retired_.push_back({host_, dev_});  // still referenced by queued copies / launches
+    size_t nc = std::max<size_t>(1 << 20, 2 * need);
+    LC(hipHostMalloc((void**)&host_, nc, hipHostMallocDefault));
+    LC(hipMalloc((void**)&dev_, nc));
+    cap_ = nc;
+    off_ = 0;
+  }
+  char* h = host_ + off_;
+  char* d = dev_ + off_;
+  std::memcpy(h, p, bytes);
+  LC(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st_));
+  off_ = (off_ + bytes + 255) & ~(size_t)255;
+  return d;
+}
+
+void gemm(Stager& S, hipStream_t st, bool ta, bool tb, const std::vector<Gemm>& g) {
+  std::vector<Gemm> live;
+  int tiles = 0;
+  for (const Gemm& x : g)
+    if (x.m > 0 && x.n > 0) {
+      live.push_back(x);
+      tiles = std::max(tiles, ((x.m + GT - 1) / GT) * ((x.n + GT - 1) / GT));
+    }
+  if (live.empty()) return;
+  const Gemm* dg = S.put(live);
+  dim3 grid((unsigned)tiles, (unsigned)live.size());
+  if (ta && tb) hipLaunchKernelGGL((k_gemm<true, true>), grid, dim3(256), 0, st, dg);
+  else if (ta) hipLaunchKernelGGL((k_gemm<true, false>), grid, dim3(256), 0, st, dg);
+  else if (tb) hipLaunchKernelGGL((k_gemm<false, true>), grid, dim3(256), 0, st, dg);
+  else hipLaunchKernelGGL((k_gemm<false, false>), grid, dim3(256), 0, st, dg);
+  LC(hipGetLastError());
+}
+
+void gemv(Stager& S, hipStream_t st, bool trans, const std::vector<Gemv>& g) {
+  std::vector<Gemv> live;
+  int outs = 0;
+  for (const Gemv& x : g)
+    if (x.m > 0 && x.n > 0) {
+      live.push_back(x);
+      outs = std::max(outs, trans ? x.n : x.m);
+    }
+  if (live.empty()) return;
+  const Gemv* dg = S.put(live);
+  if (trans)
+    hipLaunchKernelGGL(k_gemv<true>, dim3((unsigned)((outs + 3) / 4), (unsigned)live.size()), dim3(256), 0, st, dg);
+  else
+    hipLaunchKernelGGL(k_gemv<false>, dim3((unsigned)((outs + 255) / 256), (unsigned)live.size()), dim3(256), 0,
+                       st, dg);
+  LC(hipGetLastError());
+}
+
+void cholesky(Stager& S, hipStream_t st, const std::vector<Chol>& cs) {
+  if (cs.empty()) return;
+  int Mmax = 0;
+  for (const Chol& c : cs) Mmax = std::max(Mmax, c.M);
+  const Chol* dc = S.put(cs);
+  for (int jb = 0; jb < Mmax; jb += 64) {
+    hipLaunchKernelGGL(k_potrf_tile, dim3((unsigned)cs.size()), dim3(64), 0, st, dc, jb);
+    LC(hipGetLastError());
+    std::vector<Gemm> pan, upd;
+    for (const Chol& c : cs) {
+      if (c.M <= jb + 64) continue;
+      const int rest = c.M - jb - 64;
+      double* colj = c.A + (jb + 64) + (size_t)c.lda * jb;
+      // L(jb+64:, jb) = A(jb+64:, jb) Dinv_jj^T (in place: each output tile reads only its own rows)
+      pan.push_back(Gemm{colj, c.dinv + (size_t)(jb / 64) * 4096, colj, rest, 64, 64, c.lda, 64, c.lda, 1.0, 0.0, 0});
+      // A(jb+64:, jb+64:) -= L L^T, lower tiles
+      upd.push_back(Gemm{colj, colj, c.A + (jb + 64) + (size_t)c.lda * (jb + 64), rest, rest, 64, c.lda, c.lda,
+                         c.lda, -1.0, 1.0, 1});
+    }
+    gemm(S, st, false, true, pan);
+    gemm(S, st, false, true, upd);
+  }
+}
+
+void trsm_right_lt(Stager& S, hipStream_t st, const std::vector<TrsmRLT>& ts) {
+  int Mmax = 0;
+  for (const TrsmRLT& x : ts) Mmax = std::max(Mmax, x.M);
+  for (int jb = 0; jb < Mmax; jb += 64) {
+    std::vector<Gemm> sc, up;
+    for (const TrsmRLT& x : ts) {
+      if (x.M <= jb) continue;
+      const int nbj = std::min(64, x.M - jb);
+      double* Xj = x.X + (size_t)x.ldx * jb;
+      // X(:, jb) <- X(:, jb) Dinv_jj^T (in place)
+      sc.push_back(Gemm{Xj, x.dinv + (size_t)(jb / 64) * 4096, Xj, x.m, nbj, nbj, x.ldx, 64, x.ldx, 1.0, 0.0, 0});
+      if (x.M > jb + 64)  // X(:, jb+64:) -= X(:, jb) L(jb+64:, jb)^T
+        up.push_back(Gemm{Xj, x.L + (jb + 64) + (size_t)x.ldl * jb, x.X + (size_t)x.ldx * (jb + 64), x.m,
+                          x.M - jb - 64, 64, x.ldx, x.ldl, x.ldx, -1.0, 1.0, 0});
+    }
+    gemm(S, st, false, true, sc);
+    gemm(S, st, false, true, up);
+  }
+}
+
+void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es) {
+  if (es.empty()) return;
+  int Mmax = 0;
+  for (const Eigh& e : es) Mmax = std::max(Mmax, e.M);
+  if (Mmax > 4096) throw LinalgErr{"eigh: M > 4096 not supported"};
+  const Eigh* de = S.put(es);
+  const unsigned n = (unsigned)es.size();
+  const size_t lds_sy = ((size_t)(SY_W + 2) * Mmax + 64 + 2 * TNB + TNB * TNB) * sizeof(double);
+  if (lds_sy > 160 * 1024) throw LinalgErr{"eigh: matrix too large for the tridiagonalisation's LDS"};
+  hipLaunchKernelGGL(k_sytrd, dim3(n), dim3(SY_T), lds_sy, st, de);
+  LC(hipGetLastError());
+  hipLaunchKernelGGL(k_stebz_stein, dim3(n), dim3(1024), (2 * (size_t)Mmax + 64) * sizeof(double), st, de);
+  LC(hipGetLastError());
+  // BCGS2 over panels of TNB eigenvectors (columns of Z = E.A)
+  for (int p = 0; p < Mmax; p += TNB) {
+    if (p > 0) {
+      for (int pass = 0; pass < 2; ++pass) {
+        std::vector<Gemm> h, u;
+        for (const Eigh& e : es) {
+          if (e.M <= p) continue;
+          EighWs w = carve(e.work, e.M);
+          const int nb = std::min(TNB, e.M - p);
+          // H = Z(:, :p)' Z(:, p:p+nb)   (p x nb, ld M)
+          h.push_back(Gemm{e.A, e.A + (size_t)e.lda * p, w.H, p, nb, e.M, e.lda, e.lda, e.M, 1.0, 0.0, 0});
+          // Z(:, p:p+nb) -= Z(:, :p) H
+          u.push_back(Gemm{e.A, w.H, e.A + (size_t)e.lda * p, e.M, nb, p, e.lda, e.M, e.lda, -1.0, 1.0, 0});
+        }
+        gemm(S, st, true, false, h);
+        gemm(S, st, false, false, u);
+      }
+    }
+    hipLaunchKernelGGL(k_mgs_panel, dim3(n), dim3(MG_T), 0, st, de, p);
+    LC(hipGetLastError());
+  }
+  // back-transform: Z <- (I - V_p T_p V_p') Z for the panels in reverse order
+  const int npan = (Mmax - 1 + TNB - 1) / TNB;
+  for (int pi = npan - 1; pi >= 0; --pi) {
+    const int p = pi * TNB;
+    std::vector<Gemm> g1, g2, g3;
+    for (const Eigh& e : es) {
+      if (e.M - 1 <= p) continue;
+      EighWs w = carve(e.work, e.M);
+      const int nb = std::min(TNB, e.M - 1 - p), rows = e.M - p - 1;  // v rows p+1 .. M-1
+      const double* Vp = w.Vc + (size_t)e.M * p + (p + 1);
+      // X = V_p' Z(p+1:, :)   (nb x M)
+      g1.push_back(Gemm{Vp, e.A + (p + 1), w.X, nb, e.M, rows, e.M, e.lda, TNB, 1.0, 0.0, 0});
+      // Y = T_p X
+      g2.push_back(Gemm{w.T + (size_t)pi * TNB * TNB, w.X, w.Y, nb, e.M, nb, TNB, TNB, TNB, 1.0, 0.0, 0});
+      // Z(p+1:, :) -= V_p Y
+      g3.push_back(Gemm{Vp, w.Y, e.A + (p + 1), rows, e.M, nb, e.M, TNB, e.lda, -1.0, 1.0, 0});
+    }
+    gemm(S, st, true, false, g1);
+    gemm(S, st, false, false, g2);
+    gemm(S, st, false, false, g3);
+  }
+}
+
+}  // namespace oila

@@ -6,13 +6,13 @@
 // with np.random.seed(20); the caller passes them), Matern-3/2 kernel:
 //
 //   Kmm = K(x_sel, x_sel)            Knm = K(x, x_sel)            (kernels below)
-//   s, u = eigh(Kmm); s[s<=0] = 1e-12; st = n s / M               (rocSOLVER syevd)
-//   ut = sqrt(M/n) Knm u / s;  C = Vi ut = ut / sn2                (rocBLAS gemm + kernel)
-//   B = diag(1/st) + ut' C;  L = chol(B)                           (gemm + potrf)
+//   s, u = eigh(Kmm); s[s<=0] = 1e-12; st = n s / M               (oila::eigh)
+//   ut = sqrt(M/n) Knm u / s;  C = Vi ut = ut / sn2                (oila::gemm + kernel)
+//   B = diag(1/st) + ut' C;  L = chol(B)                           (oila::gemm + cholesky)
 //
 // NB1 then forms alpha = L'^-1 L^-1 C' and Ki = Vi - C alpha (n x n).  Here
-// the same quantities come from W' = C L^-T (n x M: batched trtri of L, then
-// one GEMM -- rocBLAS trsm at these shapes runs at a few TFLOP/s):
+// the same quantities come from W' = C L^-T (n x M: a right-looking block
+// triangular solve with the Cholesky's diagonal-block inverses):
 //   C alpha = W'W,  A = Ki r = r/sn2 - W'(W r),  k*'Ki k* = |k*|^2/sn2 - |W k*|^2
 // and, because D B D = H / sn2 for D = diag(sqrt(st)) and NB1's
 // H = sn2 I + (sqrt(st) ut)'(sqrt(st) ut),
@@ -27,14 +27,14 @@
 //   (exact K, dK: NB1 SMLII quirks kept)
 //   predict: fs = mean + k*.A;  sd = sqrt(sf2 - k*'Ki k*);  prior sd = sqrt(sf2)
 //
-// The dense factorisations are plain library LAPACK / GEMM (rocSOLVER /
-// rocBLAS).  rocSOLVER's syevd at M ~ 1000 is a long chain of small kernels
-// (~20 ms, latency-bound), so the cells of a call are dealt over several
-// LANES -- each its own stream, rocBLAS handle and workspace -- that run
-// concurrently; per-cell status comes back in one copy at the end.
+// Every dense step -- the eigendecomposition, the Cholesky, the products --
+// is a hand-written gfx950 kernel of oi_linalg.hip (no LAPACK / rocSOLVER /
+// rocBLAS): the eigensolver is one workgroup per matrix for the Householder
+// tridiagonalisation and the tridiagonal eigenpairs, batched MFMA products for
+// the orthogonalisation and the back-transform.  Cells of a call are dealt
+// over LANES (own stream and workspace); per-cell status comes back in one
+// copy at the end.
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <cmath>
@@ -47,6 +47,7 @@
 
 #include "../../include/oi.h"
 #include "oi_gemm.h"
+#include "oi_linalg.h"
 
 #pragma clang fp contract(off)
 
@@ -180,13 +181,6 @@ __global__ void __launch_bounds__(256) k_nys_logdet(const double* __restrict__ L
   }
   block_sum<2>(v, red);
   if (threadIdx.x == 0) res[b * strideR + 1] = v[0] + v[1] / 2.0;
-}
-
-// zero the strict upper triangle of a column-major M x M matrix (leading
-// dimension ld; potrf / trtri leave the caller's upper triangle in place)
-__global__ void k_nys_zero_upper(double* __restrict__ A, int64_t M, int64_t ld) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
-  if (i < j && j < M) A[i + ld * j] = 0.0;
 }
 
 // pad the M x M matrix in the top-left of an Mp x Mp column-major buffer to a
@@ -348,21 +342,7 @@ struct HipErr {
     hipError_t e_ = (expr);                                                                   \
     if (e_ != hipSuccess) throw HipErr{std::string(#expr) + ": " + hipGetErrorString(e_)};    \
   } while (0)
-#define BC(expr)                                                                              \
-  do {                                                                                        \
-    rocblas_status s_ = (expr);                                                               \
-    if (s_ != rocblas_status_success)                                                         \
-      throw HipErr{std::string(#expr) + ": " + rocblas_status_to_string(s_)};                 \
-  } while (0)
 #define KCHK() HC(hipGetLastError())
-
-struct Handle {
-  rocblas_handle h = nullptr;
-  Handle() { BC(rocblas_create_handle(&h)); }
-  ~Handle() {
-    if (h) rocblas_destroy_handle(h);
-  }
-};
 
 // opts.profile: HIP events around each stage of each cell, summed per stage
 // into oi_profile_json (algorithmic flops / bytes per stage alongside)
@@ -421,7 +401,7 @@ inline unsigned blocks(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 // per-cell device results: [r.A, sum log diag(L) + sum log st / 2, g0..g4 raw
 // sums, k*.A, |k*|^2, |W k*|^2]
 constexpr int NRES = 10;
-// per-cell rocSOLVER infos: [syevd, potrf(B)]
+// per-cell infos: [eigh, potrf(B)] (LAPACK's info semantics)
 constexpr int NINFO = 2;
 
 }  // namespace
@@ -484,17 +464,25 @@ struct CellOut {
   int status;
 };
 
-// One lane: a stream, a rocBLAS handle and the workspace for the largest cell.
+// Device buffer; stream-ordered (hipMallocAsync / hipFreeAsync on `st`) when
+// given a stream, so freeing it never waits for the whole device.
 struct Buf {
   void* p = nullptr;
+  hipStream_t st = nullptr;
+  bool async = false;
   Buf() = default;
   Buf(const Buf&) = delete;
   Buf& operator=(const Buf&) = delete;
   void alloc(size_t bytes) {
     if (bytes) HC(hipMalloc(&p, bytes));
   }
+  void alloc_async(size_t bytes, hipStream_t s) {
+    st = s;
+    async = true;
+    if (bytes) HC(hipMallocAsync(&p, bytes, s));
+  }
   ~Buf() {
-    if (p) (void)hipFree(p);
+    if (p) (void)(async ? hipFreeAsync(p, st) : hipFree(p));
   }
   template <class T>
   T* as() const {
@@ -504,27 +492,31 @@ struct Buf {
 
 // Device copy of one validated batch (inputs when they came from the host,
 // inducing rows, targets) and its rows of the cell table.
+// Allocated and filled on stream `st` (stream-ordered; the constructor
+// returns once the copies are done) and freed on it: a session orders `st`
+// after every group's last use before dropping a batch.
 struct BatchDev {
   Buf hx, hy, dsel, dxs;
   std::vector<CellSrc> rows;
-  BatchDev(const Batch& b, const double* xs, bool device_inputs) {
+  BatchDev(const Batch& b, const double* xs, bool device_inputs, hipStream_t st) {
     const int64_t N = b.offs[b.ncell], S = b.soffs[b.ncell];
     const double* dx = b.xyt;
     const double* dy = b.y;
     if (!device_inputs) {
-      hx.alloc(N * 3 * 8);
-      hy.alloc(N * 8);
-      HC(hipMemcpy(hx.p, b.xyt, N * 3 * 8, hipMemcpyHostToDevice));
-      HC(hipMemcpy(hy.p, b.y, N * 8, hipMemcpyHostToDevice));
+      hx.alloc_async(N * 3 * 8, st);
+      hy.alloc_async(N * 8, st);
+      HC(hipMemcpyAsync(hx.p, b.xyt, N * 3 * 8, hipMemcpyHostToDevice, st));
+      HC(hipMemcpyAsync(hy.p, b.y, N * 8, hipMemcpyHostToDevice, st));
       dx = hx.as<double>();
       dy = hy.as<double>();
     }
-    dsel.alloc(S * 8);
-    HC(hipMemcpy(dsel.p, b.sel, S * 8, hipMemcpyHostToDevice));
+    dsel.alloc_async(S * 8, st);
+    HC(hipMemcpyAsync(dsel.p, b.sel, S * 8, hipMemcpyHostToDevice, st));
     if (xs) {
-      dxs.alloc(b.ncell * 3 * 8);
-      HC(hipMemcpy(dxs.p, xs, b.ncell * 3 * 8, hipMemcpyHostToDevice));
+      dxs.alloc_async(b.ncell * 3 * 8, st);
+      HC(hipMemcpyAsync(dxs.p, xs, b.ncell * 3 * 8, hipMemcpyHostToDevice, st));
     }
+    HC(hipStreamSynchronize(st));  // host arrays may go away once submit returns
     rows.resize(b.ncell);
     for (int64_t c = 0; c < b.ncell; ++c)
       rows[c] = CellSrc{dx + b.offs[c] * 3, dy + b.offs[c], dsel.as<int64_t>() + b.soffs[c],
@@ -534,7 +526,7 @@ struct BatchDev {
 };
 
 // objective pass: fused MFMA kernel (default) or, with OI_NYS_FUSED=0, the
-// rocBLAS GEMM forming Ki followed by k_nys_grad
+// n x n product forming Ki (oila::gemm) followed by k_nys_grad
 inline bool fused_objective() {
   const char* e = getenv("OI_NYS_FUSED");
   return !(e && atoi(e) == 0);
@@ -542,14 +534,14 @@ inline bool fused_objective() {
 
 struct Lane {
   hipStream_t st = nullptr;
-  Handle H;
+  oila::Stager la;  // launch descriptors of the oila kernels on this lane's stream
   Buf Knm, U1, ut, W, Ki, Wp, Av, tv, ks, kv, xsc, part;
   Stager sg;
   hipEvent_t done = nullptr;
   Lane(int64_t nmax, int64_t mmax, bool obj, bool pred, bool profile) {
     HC(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     HC(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-    BC(rocblas_set_stream(H.h, st));
+    la.bind(st);
     const int64_t nM = nmax * mmax, nt = blocks(nmax, 64);
     Knm.alloc(nM * 8);
     U1.alloc(nM * 8);
@@ -581,13 +573,12 @@ struct Lane {
 
 // Evaluates any subset of a validated batch's cells at given LINEAR hypers.
 //
-// rocSOLVER's syevd / potrf at M ~ 1000 are long chains of small kernels
-// (~20 ms / ~2.4 ms for one matrix, latency-bound); their strided-batched
-// forms factor 8 such matrices in ~1.4x the time of one.  So a run is
-// phase-major over CHUNKS of cells (sorted by M, so equal-M cells are
-// adjacent slots): (1) K_mm of every cell, (2) one batched syevd per equal-M
-// group, (3) the n x M panels and B of every cell, (4) one batched potrf per
-// group, (5) the triangular solve, objective and prediction of every cell.
+// The eigensolver runs one workgroup per matrix and the blocked Cholesky one
+// launch sequence for many matrices, so a run is phase-major over CHUNKS of
+// cells (sorted by M): (1) K_mm of every cell, (2) one batched eigh per
+// equal-padded-M group, (3) the n x M panels and B of every cell, (4) one
+// batched Cholesky per group, (5) the triangular solve, objective and
+// prediction of every cell.
 // Per-cell phases are dealt round-robin over LANES (OI_NYS_LANES, default 1:
 // stream + rocBLAS handle + scratch each; more lanes measured no faster with
 // the box's 4 hardware queues); per-slot state (scaled inputs,
@@ -607,10 +598,10 @@ class Runner {
       own_ = true;
     }
     res_.alloc(cap * NRES * 8);
-    info_.alloc(cap * NINFO * sizeof(rocblas_int));
+    info_.alloc(cap * NINFO * sizeof(int32_t));
     HC(hipHostMalloc((void**)&hr_, cap * NRES * 8, hipHostMallocDefault));
-    HC(hipHostMalloc((void**)&hi_, cap * NINFO * sizeof(rocblas_int), hipHostMallocDefault));
-    BC(rocblas_set_stream(H_.h, st_));
+    HC(hipHostMalloc((void**)&hi_, cap * NINFO * sizeof(int32_t), hipHostMallocDefault));
+    la_.bind(st_);
     sg_.on = o.profile != 0;
     sg_.st = st_;
     int nl = 1;
@@ -619,16 +610,19 @@ class Runner {
     nl = nl > cap ? (int)cap : nl;
     for (int l = 0; l < nl; ++l)
       lanes_.emplace_back(new Lane(nmax, mmax, want_obj, want_pred, o.profile != 0));
-    // padding quantum for the batched factorisations (OI_NYS_PAD, default 32;
-    // 0 = batch only cells of equal M): K_mm and B of a cell are factored as
-    // diag(A, d I) of size Mp = M rounded up, so cells of different M share
-    // one strided-batched call
+    // padding quantum (OI_NYS_PAD, default 32; 0 = no padding): K_mm and B of a
+    // cell are factored as diag(A, d I) of size Mp = M rounded up (the slot
+    // strides of the chunk arrays; results equal the unpadded path to rounding)
     if (const char* e = getenv("OI_NYS_PAD")) padq_ = std::max(0, atoi(e));
     mpmax_ = Mp(mmax);
-    // slot arrays: sc, sq (n x 3), Kmm (Mp^2), s, st, E (Mp), C (n x M), B (Mp^2);
+    // slot arrays: sc, sq (n x 3), Kmm (Mp^2), s, st (Mp), C (n x M), B (Mp^2),
+    // the eigensolver's workspace, the Cholesky's diagonal-block inverses;
     // chunk <= 64 cells and <= 1/4 of the free HBM
     const int64_t mmaxp = mpmax_;
-    const size_t per = (size_t)(6 * nmax + 2 * mmaxp * mmaxp + 3 * mmaxp + nmax * mmaxp) * 8;
+    ewd_ = oila::eigh_workspace_doubles((int)mmaxp);
+    nd64_ = (mmaxp + 63) / 64;
+    const size_t per = (size_t)(6 * nmax + 2 * mmaxp * mmaxp + 2 * mmaxp + nmax * mmaxp) * 8 +
+                       (ewd_ + (size_t)nd64_ * 4096) * 8;
     size_t fr = 0, tot = 0;
     HC(hipMemGetInfo(&fr, &tot));
     int64_t ch = std::min<int64_t>(64, cap);
@@ -639,10 +633,10 @@ class Runner {
     Kmm_.alloc(ch * mmaxp * mmaxp * 8);
     eval_.alloc(ch * mmaxp * 8);
     stl_.alloc(ch * mmaxp * 8);
-    E_.alloc(ch * mmaxp * 8);
     C_.alloc(ch * nmax * mmaxp * 8);
     B_.alloc(ch * mmaxp * mmaxp * 8);
-    info_tmp_.alloc(2 * ch * sizeof(rocblas_int));
+    EW_.alloc(ch * ewd_ * 8);
+    Dinv_.alloc(ch * nd64_ * 4096 * 8);
     HC(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   }
   ~Runner() {
@@ -684,7 +678,7 @@ class Runner {
       return Mof(cells[a]) < Mof(cells[c]);
     });
     HC(hipMemsetAsync(res_.p, 0, nc * NRES * 8, st_));
-    HC(hipMemsetAsync(info_.p, 0, nc * NINFO * sizeof(rocblas_int), st_));
+    HC(hipMemsetAsync(info_.p, 0, nc * NINFO * sizeof(int32_t), st_));
     for (int64_t p0 = 0; p0 < nc; p0 += chunk_) {
       const int64_t p1 = std::min(nc, p0 + chunk_);
       lanes_phase(p0, p1, 1);
@@ -694,7 +688,7 @@ class Runner {
       lanes_phase(p0, p1, 5);
     }
     HC(hipMemcpyAsync(hr_, res_.p, nc * NRES * 8, hipMemcpyDeviceToHost, st_));
-    HC(hipMemcpyAsync(hi_, info_.p, nc * NINFO * sizeof(rocblas_int), hipMemcpyDeviceToHost, st_));
+    HC(hipMemcpyAsync(hi_, info_.p, nc * NINFO * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
   }
 
   // wait for the queued evaluation; out[k] for the enqueued cells[k]
@@ -707,13 +701,15 @@ class Runner {
     HC(hipStreamSynchronize(st_));
     sg_.flush();
     for (Lane* l : lanes_) l->sg.flush();
+    la_.reset();  // every launch that read the staged descriptors has completed
+    for (Lane* l : lanes_) l->la.reset();
     const double inf = INFINITY, nan = NAN;
     for (int64_t p = 0; p < nc; ++p) {
       const int64_t k = order_[p], c = cells[k];
       const int64_t n = (*tab_)[c].n, M = Mof(c);
       const double sf2 = hyp[k * 5 + 3], sn2 = hyp[k * 5 + 4];
       const double* rr = hr_ + p * NRES;
-      const rocblas_int* ii = hi_ + p * NINFO;
+      const int32_t* ii = hi_ + p * NINFO;
       const bool bad = ii[0] != 0 || ii[1] != 0;  // NB1's LinAlgError (eigh / cholesky)
       CellOut& r = out[k];
       r.status = bad ? 1 : 0;
@@ -763,8 +759,10 @@ class Runner {
     }
   }
 
-  // which = 0: s, u = eigh(Kmm) (syevd); 1: L = chol(B) (potrf) -- one
-  // strided-batched call per run of slots with equal padded size, on the main stream
+  // which = 0: s, u = eigh(Kmm) (oila::eigh; u overwrites Kmm); 1: L = chol(B)
+  // (oila::cholesky, in place, with the diagonal-block inverses kept for the
+  // triangular solve) -- one batched call per run of slots with equal padded
+  // size, on the main stream
   void batched(int64_t p0, int64_t p1, int which) {
     const int64_t mm = mpmax_ * mpmax_;
     for (int64_t g0 = p0; g0 < p1;) {
@@ -773,35 +771,32 @@ class Runner {
       while (g1 < p1 && Mp(Mof((*cells_)[order_[g1]])) == M) ++g1;
       const int iM = (int)M, cnt = (int)(g1 - g0);
       const int64_t s0 = g0 - p0;
-      rocblas_int* inf = info_.as<rocblas_int>() + g0 * NINFO + which;
-      // info of slot q lands at info_[(g0+q)*NINFO + which]: stride NINFO ints,
-      // so the batched call writes into a contiguous scratch and a copy spreads it
-      rocblas_int* tmp = info_tmp_.as<rocblas_int>();  // chunk_ >= cnt entries
       const double dM = (double)M;
       if (which == 0) {
         sg_.begin(S_EIGH, 4.0 * dM * dM * dM * cnt, 0.0);
-        BC(rocsolver_dsyevd_strided_batched(H_.h, rocblas_evect_original, rocblas_fill_lower, iM,
-                                            Kmm_.as<double>() + s0 * mm, iM, mm,
-                                            eval_.as<double>() + s0 * mpmax_, mpmax_,
-                                            E_.as<double>() + s0 * mpmax_, mpmax_, tmp, cnt));
+        std::vector<oila::Eigh> es;
+        for (int q = 0; q < cnt; ++q)
+          es.push_back(oila::Eigh{Kmm_.as<double>() + (s0 + q) * mm, eval_.as<double>() + (s0 + q) * mpmax_,
+                                  EW_.as<double>() + (s0 + q) * ewd_, iM, iM});
+        oila::eigh(la_, st_, es);
         sg_.end();
       } else {
-        // L = chol(B); half log-determinants; L^-1 in place (the lanes then form
-        // W' = C L^-T with one GEMM instead of a triangular solve)
-        sg_.begin(S_PANEL, 2.0 * dM * dM * dM / 3 * cnt, 0.0);
+        // L = chol(B); half log-determinants (the lanes then form W' = C L^-T
+        // by a block triangular solve with the kept diagonal-block inverses)
+        sg_.begin(S_PANEL, dM * dM * dM / 3 * cnt, 0.0);
         double* B0 = B_.as<double>() + s0 * mm;
-        BC(rocsolver_dpotrf_strided_batched(H_.h, rocblas_fill_lower, iM, B0, iM, mm, tmp, cnt));
+        std::vector<oila::Chol> cs;
+        for (int q = 0; q < cnt; ++q)
+          cs.push_back(oila::Chol{B0 + q * mm, Dinv_.as<double>() + (s0 + q) * nd64_ * 4096,
+                                  info_.as<int32_t>() + (g0 + q) * NINFO + 1, iM, iM});
+        oila::cholesky(la_, st_, cs);
         // the pad block is the identity: log 1 = 0 and st is 1 there (see phase3)
         hipLaunchKernelGGL(k_nys_logdet, dim3(cnt), dim3(256), 0, st_, B0, M, M, mm,
                            stl_.as<double>() + s0 * mpmax_, mpmax_,
                            res_.as<double>() + g0 * NRES, (int64_t)NRES);
         KCHK();
-        BC(rocsolver_dtrtri_strided_batched(H_.h, rocblas_fill_lower, rocblas_diagonal_non_unit, iM,
-                                            B0, iM, mm, tmp + cnt, cnt));
         sg_.end();
       }
-      HC(hipMemcpy2DAsync(inf, NINFO * sizeof(rocblas_int), tmp, sizeof(rocblas_int),
-                          sizeof(rocblas_int), cnt, hipMemcpyDeviceToDevice, st_));
       g0 = g1;
     }
   }
@@ -814,7 +809,7 @@ class Runner {
     const double* r;
     const int64_t* sl;
     const double* hp;
-    double *sc, *sq, *Kmm, *s, *stl, *C, *B, *rs;
+    double *sc, *sq, *Kmm, *s, *stl, *C, *B, *rs, *dinv;
   };
   CellRefs refs(int64_t p, int64_t slot) {
     CellRefs R;
@@ -841,6 +836,7 @@ class Runner {
     R.C = C_.as<double>() + slot * nmax * mmax;
     R.B = B_.as<double>() + slot * mmax * mmax;
     R.rs = res_.as<double>() + p * NRES;
+    R.dinv = Dinv_.as<double>() + slot * nd64_ * 4096;
     return R;
   }
 
@@ -870,8 +866,6 @@ class Runner {
   void phase3(Lane& L, int64_t p, int64_t slot) {
     const CellRefs R = refs(p, slot);
     hipStream_t st = L.st;
-    rocblas_handle h = L.H.h;
-    const double one = 1.0, zero = 0.0;
     double* Knm = L.Knm.as<double>();
     double* U1 = L.U1.as<double>();
     double* ut = L.ut.as<double>();
@@ -882,13 +876,13 @@ class Runner {
     hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
                        nullptr, R.n, R.sc, R.sl, R.hp[3], Knm, R.n);
     KCHK();
-    BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, R.in, R.iM, R.iM, &one, Knm,
-                     R.in, R.Kmm, R.iMp, &zero, U1, R.in));
+    // U1 = Knm u
+    oila::gemm(L.la, st, false, false, {oila::Gemm{Knm, R.Kmm, U1, R.in, R.iM, R.iM, R.in, R.iMp, R.in, 1.0, 0.0, 0}});
     hipLaunchKernelGGL(k_nys_ut, dim3(blocks(R.n * R.M, 256)), dim3(256), 0, st, U1, R.n, R.M, R.s,
                        std::sqrt(R.dM / R.dn), 1.0 / R.hp[4], ut, R.C);
     KCHK();
-    BC(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, R.iM, R.iM, R.in, &one,
-                     ut, R.in, R.C, R.in, &zero, R.B, R.iMp));
+    // B = ut' C (then + diag(1/st))
+    oila::gemm(L.la, st, true, false, {oila::Gemm{ut, R.C, R.B, R.iM, R.iM, R.in, R.in, R.in, R.iMp, 1.0, 0.0, 0}});
     hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.B, R.M, R.Mp, R.stl, 1,
                        0.0);
     KCHK();
@@ -904,8 +898,6 @@ class Runner {
   void phase5(Lane& L, int64_t p, int64_t slot) {
     const CellRefs R = refs(p, slot);
     hipStream_t st = L.st;
-    rocblas_handle h = L.H.h;
-    const double one = 1.0, zero = 0.0, mone = -1.0;
     const double sf2 = R.hp[3], isn2 = 1.0 / R.hp[4];
     const double dn = R.dn, dM = R.dM;
     double* Wt = L.W.as<double>();  // n x M
@@ -913,16 +905,13 @@ class Runner {
     double* tv = L.tv.as<double>();
     Stager& sg = L.sg;
     sg.begin(S_APPLY, 2.0 * dM * dM * dn + 4.0 * dn * dM, 16.0 * dn * dM);
-    hipLaunchKernelGGL(k_nys_zero_upper, dim3(blocks(R.M, 256), (unsigned)R.M), dim3(256), 0, st,
-                       R.B, R.M, R.Mp);
-    KCHK();
-    BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.iM, R.iM, &one,
-                     R.C, R.in, R.B, R.iMp, &zero, Wt, R.in));
+    // W' = C L^-T: copy C, then the right-looking block triangular solve
+    HC(hipMemcpyAsync(Wt, R.C, (size_t)R.n * R.M * 8, hipMemcpyDeviceToDevice, st));
+    oila::trsm_right_lt(L.la, st, {oila::TrsmRLT{Wt, R.B, R.dinv, R.in, R.iM, R.in, R.iMp}});
     hipLaunchKernelGGL(k_nys_vi, dim3(blocks(R.n, 256)), dim3(256), 0, st, R.r, R.n, isn2, Av);
     KCHK();
-    BC(rocblas_dgemv(h, rocblas_operation_transpose, R.in, R.iM, &one, Wt, R.in, R.r, 1, &zero, tv,
-                     1));
-    BC(rocblas_dgemv(h, rocblas_operation_none, R.in, R.iM, &mone, Wt, R.in, tv, 1, &one, Av, 1));
+    oila::gemv(L.la, st, true, {oila::Gemv{Wt, R.r, tv, R.in, R.iM, R.in, 1.0, 0.0}});     // tv = W r
+    oila::gemv(L.la, st, false, {oila::Gemv{Wt, tv, Av, R.in, R.iM, R.in, -1.0, 1.0}});   // A -= W' tv
     sg.end();
     if (obj_) {
       double* Ki = L.Ki.as<double>();
@@ -952,8 +941,7 @@ class Runner {
         // Ki = Vi - W'W (full GEMM: rocBLAS dsyrk at this shape is ~2x slower than
         // dgemm although it does half the flops; the sweep below reads the lower half)
         sg.begin(S_KI, 2.0 * dn * dn * dM, 8.0 * dn * dn);
-        BC(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, R.in, R.in, R.iM,
-                         &mone, Wt, R.in, Wt, R.in, &zero, Ki, R.in));
+        oila::gemm(L.la, st, false, true, {oila::Gemm{Wt, Wt, Ki, R.in, R.in, R.iM, R.in, R.in, R.in, -1.0, 0.0, 0}});
         hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.n, 256)), dim3(256), 0, st, Ki, R.n, R.n, nullptr,
                            0, isn2);
         KCHK();
@@ -985,8 +973,7 @@ class Runner {
       KCHK();
       hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, ks, ks, R.n, R.rs + 8);
       KCHK();
-      BC(rocblas_dgemv(h, rocblas_operation_transpose, R.in, R.iM, &one, Wt, R.in, ks, 1, &zero, kv,
-                       1));
+      oila::gemv(L.la, st, true, {oila::Gemv{Wt, ks, kv, R.in, R.iM, R.in, 1.0, 0.0}});  // kv = W k*
       hipLaunchKernelGGL(k_nys_dot, dim3(1), dim3(256), 0, st, kv, kv, R.M, R.rs + 9);
       KCHK();
       sg.end();
@@ -998,11 +985,13 @@ class Runner {
   hipStream_t st_;
   bool obj_ = false, pred_ = false, alloc_obj_, alloc_pred_;
   Buf res_, info_;
-  Buf sc_, sq_, Kmm_, eval_, stl_, E_, C_, B_, info_tmp_;
+  Buf sc_, sq_, Kmm_, eval_, stl_, C_, B_, EW_, Dinv_;
   int64_t chunk_ = 1;
   int padq_ = 32;
   int64_t mpmax_ = 0;
-  Handle H_;
+  size_t ewd_ = 0;
+  int64_t nd64_ = 0;
+  oila::Stager la_;
   Stager sg_;
   std::vector<Lane*> lanes_;
   hipEvent_t ready_ = nullptr;
@@ -1015,7 +1004,7 @@ class Runner {
   double mean_ = 0.0;
   bool own_ = false;
   double* hr_ = nullptr;       // pinned: the result copies stay asynchronous
-  rocblas_int* hi_ = nullptr;
+  int32_t* hi_ = nullptr;
 };
 
 template <class F>
@@ -1023,6 +1012,8 @@ int guarded(F&& f) {
   try {
     return f();
   } catch (const HipErr& e) {
+    return oi_set_last_error(OI_E_HIP, e.msg.c_str());
+  } catch (const oila::LinalgErr& e) {
     return oi_set_last_error(OI_E_HIP, e.msg.c_str());
   } catch (const std::bad_alloc&) {
     return oi_set_last_error(OI_E_NOMEM, "allocation failed");
@@ -1049,7 +1040,7 @@ extern "C" int oi_nystrom_batch(const double* xyt, const double* y, const int64_
   oi_options o;
   if (int rc = setup(opts, o)) return rc;
   return guarded([&] {
-    BatchDev bd(b, want_pred ? xs : nullptr, o.device_inputs != 0);
+    BatchDev bd(b, want_pred ? xs : nullptr, o.device_inputs != 0, (hipStream_t)o.stream);
     Runner R(&bd.rows, b.nmax, b.mmax, ncell, o, want_obj, want_pred);
     std::vector<int64_t> cells(ncell);
     for (int64_t c = 0; c < ncell; ++c) cells[c] = c;
@@ -1116,7 +1107,7 @@ extern "C" int oi_nystrom_fit_batch(const double* xyt, const double* y, const in
     G = std::max(1, std::min<int>(G, (int)ncell));
     std::vector<std::vector<int64_t>> gcells(G);
     for (int64_t c = 0; c < ncell; ++c) gcells[c % G].push_back(c);
-    BatchDev bd(b, xs, o.device_inputs != 0);
+    BatchDev bd(b, xs, o.device_inputs != 0, (hipStream_t)o.stream);
     std::vector<std::unique_ptr<Runner>> RG;
     for (int g = 0; g < G; ++g)
       RG.emplace_back(new Runner(&bd.rows, b.nmax, b.mmax, (int64_t)gcells[g].size(), o, true, false, G > 1));
@@ -1226,10 +1217,21 @@ struct oi_nystrom_session {
   };
   std::vector<Grp> grp;
   std::unique_ptr<Runner> pred;      // predictions of completed tickets
+  // inputs of submitted batches are allocated, copied and freed on this stream
+  // (stream-ordered): dropping a completed batch never drains the groups'
+  // rounds in flight (a ticket's cells are in no round by then)
+  hipStream_t io = nullptr;
 
   ~oi_nystrom_session() {
     for (auto* p : cg)
       if (p) oi_cg_destroy(p);
+    grp.clear();
+    pred.reset();
+    tickets.clear();
+    if (io) {
+      (void)hipStreamSynchronize(io);
+      (void)hipStreamDestroy(io);
+    }
   }
 
   void build_runners(int64_t nm, int64_t mm) {
@@ -1305,7 +1307,7 @@ struct oi_nystrom_session {
       cg[t.first + k] = nullptr;
     }
     t.done = true;
-    t.dev.reset();  // device inputs of the batch are no longer read
+    t.dev.reset();  // no round reads the batch any more: freed in io-stream order
   }
 
   void admit(Grp& g) {
@@ -1366,6 +1368,11 @@ extern "C" oi_nystrom_session* oi_nystrom_session_create(const oi_options* opts)
   if (setup(opts, o)) return nullptr;
   auto* s = new oi_nystrom_session();
   s->o = o;
+  if (hipStreamCreateWithFlags(&s->io, hipStreamNonBlocking) != hipSuccess) {
+    delete s;
+    oi_set_last_error(OI_E_HIP, "hipStreamCreate failed");
+    return nullptr;
+  }
   s->maxiter = o.maxiter < 0 ? 1000 : o.maxiter;  // scipy: len(x0) * 200 for NB1's 5 hypers
   s->gtol = o.gtol;
   if (const char* e = getenv("OI_NYS_GROUPS")) s->G = std::max(1, atoi(e));
@@ -1394,7 +1401,7 @@ extern "C" int64_t oi_nystrom_session_submit(oi_nystrom_session* s, const double
     t->info = info;
     ticket = (int64_t)s->tickets.size();
     if (ncell > 0) {
-      t->dev.reset(new BatchDev(b, xs, s->o.device_inputs != 0));
+      t->dev.reset(new BatchDev(b, xs, s->o.device_inputs != 0, s->io));
       if (s->grp.empty() || b.nmax > s->nmax || b.mmax > s->mmax) {
         s->drain();  // no round in flight over the old Runners' workspaces
         s->build_runners(b.nmax, b.mmax);
