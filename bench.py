@@ -716,14 +716,13 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
     kd = kern[dom]
     achieved_exec = kd['flops'] / (kd['total_ms'] / 1e3) / 1e12 if kd['total_ms'] > 0 else 0.0
     # algorithmic flops of the dominant kernel (SURVEY §8d per-unit figures):
-    # the factor family (k_scale, k_panel_even, k_chol_panel) carries potrf +
+    # the factor family (k_panel4, k_panel_even, k_chol_panel) carries potrf +
     # trtri = 2n^3/3 per evaluation and potrf n^3/3 per predict, k_lauum_grad
     # the lauum n^3/3 per evaluation; each kernel gets its family's algorithmic
     # flops in proportion to its share of the family's executed tile products.
     fam_alg = {'factor': float(np.sum((evals * 2.0 / 3.0 + 1.0 / 3.0) * n ** 3)),
                'lauum': float(np.sum(evals * n ** 3 / 3.0))}
-    fam_of = {'k_scale': 'factor', 'k_panel_even': 'factor', 'k_panel4': 'factor', 'k_chol_panel': 'factor',
-              'k_panel_pair': 'factor',
+    fam_of = {'k_panel_even': 'factor', 'k_panel4': 'factor', 'k_chol_panel': 'factor',
               'k_lauum_grad': 'lauum'}
     fam = fam_of.get(dom)
     fam_exec = sum(v['flops'] for k, v in kern.items() if fam_of.get(k) == fam) if fam else 0.0

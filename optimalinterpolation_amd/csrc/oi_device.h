@@ -55,8 +55,6 @@ struct OiCell {
   double* L;          // packed lower tiles (T(T+1)/2 * 4096)
   double* W;          // packed lower tiles of L^-1 (eval mode), else null
   double* Dinv;       // T * 4096
-  double* P;          // P-form: T * 4096, P_jk = -Dinv_jj L_jk of the current block column; folded pair
-                      // step: 4 * 4096 scratch (E tiles 0..2, W_j+1,j column-major in tile 3)
   double* vec;        // 4 * T * 64: z | alpha | kstar | v.  z = L^-1 r and (predict)
                       // v = L^-1 k* are built in place during the factorisation
   double* part;       // partial sums, see OI_PART_*
@@ -92,22 +90,13 @@ extern "C" {
 // `list` holds indices into `cells` sorted by T descending.
 int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
-int oi_launch_scale(const OiCell* cells, const int32_t* list, int ncell, int j, int kbeg,
-                    void* stream);
-// pform = 1: the P-form panels (P_jk = -Dinv_jj L_jk from k_scale streamed in
-// the GEMM loop); 0 (default): post-form, Dinv_jj applied to the finished sum
+// the panels stream the L tiles and apply Dinv_jj to the finished sum (post-form)
 int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                         int kbeg, int with_trtri, int pform, void* stream);
+                         int kbeg, int with_trtri, void* stream);
 int oi_launch_panel4(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j, int with_trtri,
                      void* stream);
 int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                         int with_trtri, int pform, void* stream);
-// folded pair step (OI_FOLD=1): k_diag_pair(j) factors / inverts the 128 x 128
-// diagonal block (j, j+1); k_panel_pair(j) finishes both block columns (c.P: 4
-// scratch tiles per cell)
-int oi_launch_diag_pair(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
-int oi_launch_panel_pair(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j, int with_trtri,
-                         void* stream);
+                         int with_trtri, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                          void* stream);
 // flag != nullptr: the last workgroup stores seq to *flag (pinned host) once all

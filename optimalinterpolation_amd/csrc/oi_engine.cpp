@@ -108,26 +108,22 @@ class Arena {
   std::map<size_t, size_t> free_;
 };
 
-// ptiles: scratch tiles per cell -- T for the P-form panels, 4 for the folded
-// pair step (OI_FOLD), else 0
-size_t cell_bytes(int64_t n, bool eval, int ptiles) {
+size_t cell_bytes(int64_t n, bool eval) {
   const size_t T = (size_t)tiles_of(n), nt = T * (T + 1) / 2;
   size_t b = 0;
   auto add = [&](size_t x) { b += (x + 255) & ~size_t(255); };
   add(nt * OI_TILE * 8);                         // L
   if (eval) add(nt * OI_TILE * 8);               // W
   add(T * OI_TILE * 8);                          // Dinv
-  if (ptiles) add((size_t)ptiles * OI_TILE * 8);  // P (P-form: T tiles; folded pair step: 4)
   add(4 * T * OI_NB * 8);                        // vec
   add((size_t)OI_PART_SIZE(nt, T) * 8);          // part
   return b;
 }
 
 // ------------------------------------------------------------- profiling
-enum KernelId { K_BUILD, K_CHOL, K_SCALE, K_TRSM, K_EVEN, K_LAUUM, K_FINAL, K_EVEN4, K_PAIR, K_COUNT };
-const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_chol_panel",
-                                    "k_panel_even", "k_lauum_grad", "k_finalize", "k_panel4",
-                                    "k_panel_pair"};
+enum KernelId { K_BUILD, K_CHOL, K_TRSM, K_EVEN, K_LAUUM, K_FINAL, K_EVEN4, K_COUNT };
+const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_chol_panel", "k_panel_even",
+                                    "k_lauum_grad", "k_finalize", "k_panel4"};
 
 // Panel scheme, read per call from OI_PANEL:
 //   2 (default): even/odd block-column pairs share one stream (k_panel_even +
@@ -138,15 +134,6 @@ const char* kKernelName[K_COUNT] = {"k_build", "k_diag_factor", "k_scale", "k_ch
 //                whole block row of L (and of W = L^-1).
 bool legacy_panels() {
   const char* e = getenv("OI_PANEL");
-  return e && atoi(e) == 1;
-}
-// Panel form, read per call from OI_PFORM:
-//   0 (default): post-form -- the panels stream L_jk and apply Dinv_jj once to
-//                the finished sum (post_left / post_right): no k_scale launch;
-//   1          : P-form -- k_scale writes P_jk = -Dinv_jj L_jk, streamed by the
-//                panels with A_ij Dinv_jj^T as the GEMM loop's last pair.
-bool pform_panels() {
-  const char* e = getenv("OI_PFORM");
   return e && atoi(e) == 1;
 }
 // Even-column panel core, read per call from OI_PANEL4: 1 (default) => k_panel4
@@ -171,15 +158,6 @@ int panel4_minj() {
 int panel4_mint() {
   const char* e = getenv("OI_PANEL4_MINT");
   return e ? atoi(e) : 12;
-}
-// Folded pair step, read per call from OI_FOLD: 1 => k_diag_pair +
-// k_panel_pair per block-column pair (the 128 x 128 diagonal block factored
-// and inverted first, both columns of every row finished by one stream, no
-// odd-column launch); 0 (default until it measures faster) => k_diag_factor per column + k_panel4 / k_panel_even
-// (even j) + k_chol_panel (odd j).  Post-form two-column scheme only.
-bool fold_enabled() {
-  const char* e = getenv("OI_FOLD");
-  return e && atoi(e) == 1;
 }
 // Executed MFMA flops per cell and launch (profile mode), mirroring the
 // kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
@@ -275,60 +253,6 @@ double panel4(int T, int n, int j, bool eval) {
   return blocks * BLK;
 }
 
-// k_panel_pair: look-ahead slot, row pairs (+ the first pair's E products),
-// W pairs; post_pair's 128-wide triangular product per output row is
-// 4 row blocks x sum_nb (4 nb + 4) MFMAs (144 BLK units; 40 with one column)
-double panel_pair(int T, int n, int j, bool eval) {
-  const int rT = n - OI_NB * (T - 1), nrp = T - 1 - j > 0 ? (T - 1 - j) >> 1 : 0;
-  const bool has_next = j + 1 < T;
-  const double post_row = has_next ? 144.0 : 40.0;
-  double blocks = 0;
-  if (j >= 2 && j + 2 < T) {
-    const int a = j + 2, b = j + 3;
-    for (int w = 0; w < 8; ++w) {
-      const int wr = w >> 1, wc = w & 1, qr = wr >> 1;
-      unsigned skip = 0;
-      for (int mb = 0; mb < 2; ++mb)
-        for (int nb = 0; nb < 4; ++nb) {
-          const int m0 = 32 * (wr & 1) + 16 * mb, n0 = 16 * nb, ti = qr ? b : a, tj = wc ? b : a;
-          if ((qr == 0 && wc == 1) || ti >= T || tj >= T || (qr == wc && m0 + 15 < n0) ||
-              (ti == T - 1 && m0 >= rT) || (tj == T - 1 && n0 >= rT))
-            skip |= 1u << (4 * mb + nb);
-        }
-      blocks += 4.0 * j * live8(skip);
-    }
-  }
-  for (int y = 0; y < nrp; ++y) {
-    const int i1 = j + 2 + 2 * y, i2 = i1 + 1;
-    const bool masked = i2 >= T - 1 || j + 1 == T - 1;
-    for (int w = 0; w < 8; ++w) {
-      const int wr = w >> 1, wc = w & 1, ti = wr >= 2 ? i2 : i1, tj = wc ? j + 1 : j;
-      unsigned skip = 0;
-      for (int mb = 0; mb < 2; ++mb)
-        for (int nb = 0; nb < 4; ++nb) {
-          const int m0 = 32 * (wr & 1) + 16 * mb, n0 = 16 * nb;
-          if (ti >= T || (ti == T - 1 && m0 >= rT) || (tj == T - 1 && n0 >= rT)) skip |= 1u << (4 * mb + nb);
-        }
-      blocks += 4.0 * j * (masked ? live8(skip) : 8);
-    }
-    blocks += post_row * (i2 < T ? 2 : 1);
-    if (y == 0) blocks += 8.0 * 64;  // E: 8 chunks on the unmasked core
-  }
-  if (eval)
-    for (int y = 0; 2 * y < j; ++y) {
-      const bool masked = j >= T - 2;
-      for (int w = 0; w < 8; ++w) {
-        const int wc = w & 1, tj = wc ? j + 1 : j;
-        unsigned skip = 0;
-        for (int nb = 0; nb < 4; ++nb)
-          if ((wc == 1 && !has_next) || (tj == T - 1 && 16 * nb >= rT)) skip |= 0x11u << nb;
-        blocks += 4.0 * (j - 2 * y) * (masked ? live8(skip) : 8);
-      }
-      blocks += 2 * post_row;
-    }
-  return blocks * BLK;
-}
-
 double chol_panel(int T, int n, int j, int kbeg, bool eval, bool post) {
   const int rT = n - OI_NB * (T - 1), nf = T - 1 - j;
   auto factor_wg = [&](int x) {
@@ -370,14 +294,6 @@ double chol_panel(int T, int n, int j, int kbeg, bool eval, bool post) {
     }
   }
   return blocks * BLK;
-}
-
-// k_scale: per tile, B(q, n) = Dinv[n][q] is zero past the block's last column
-double scale_tile() {
-  double mfma = 0;
-  for (int wc = 0; wc < 2; ++wc)
-    for (int nb = 0; nb < 2; ++nb) mfma += 2 * 2 * std::min(16, (32 * wc + 16 * nb + 15) / 4 + 1);
-  return mfma * 2.0 * 16 * 16 * 4;
 }
 
 double lauum(int T, int n) {
@@ -608,9 +524,8 @@ struct Slot {
 class Engine {
  public:
   Engine(Context& ctx, const oi_options& o, int64_t cap_hint)
-      : ctx_(ctx), o_(o), legacy_(legacy_panels()), pform_(pform_panels()), panel4_(panel4_enabled()),
+      : ctx_(ctx), o_(o), legacy_(legacy_panels()), panel4_(panel4_enabled()),
         panel4_minj_(panel4_minj()), panel4_mint_(panel4_mint()) {
-    fold_ = fold_enabled() && !legacy_ && !pform_;
     HIPC(hipSetDevice(ctx.device));
     st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
     ss_ = ctx.sub_stream;
@@ -766,7 +681,7 @@ class Engine {
     jb.dw = d_dw;
     size_t max_cell = 0;
     for (int64_t c = 0; c < nc; ++c)
-      max_cell = std::max(max_cell, cell_bytes(jb.m[c], jb.kind != Job::PREDICT_ONLY, ptiles(jb.m[c])));
+      max_cell = std::max(max_cell, cell_bytes(jb.m[c], jb.kind != Job::PREDICT_ONLY));
     if (max_cell > ctx_.arena.size()) {
       // in_off == SIZE_MAX: the inputs went to the job's own buffer, nothing
       // of the arena to return
@@ -794,10 +709,9 @@ class Engine {
 
   bool done(int64_t id) const { return id < next_id_ && !jobs_.count(id); }
 
-  int ptiles(int64_t n) const { return pform_ ? tiles_of(n) : fold_ ? 4 : 0; }
 
   bool use_panel4(int j, int maxT) const {
-    return panel4_ && !pform_ && j >= panel4_minj_ && maxT >= panel4_mint_;
+    return panel4_ && j >= panel4_minj_ && maxT >= panel4_mint_;
   }
 
   // The stream later submissions' device inputs are ordered after (the rounds
@@ -874,7 +788,7 @@ class Engine {
       const Job& job = *jp;
       const int64_t n = job.m[c];  // the cell's problem size: its distinct sites
       const bool eval_mem = job.kind != Job::PREDICT_ONLY;
-      const size_t bytes = cell_bytes(n, eval_mem, ptiles(n));
+      const size_t bytes = cell_bytes(n, eval_mem);
       const size_t off = ctx_.arena.alloc(bytes);
       if (off == SIZE_MAX) break;
       queue_.pop_front();
@@ -901,7 +815,6 @@ class Engine {
       cd.L = take(nt * OI_TILE * 8);
       cd.W = eval_mem ? take(nt * OI_TILE * 8) : nullptr;
       cd.Dinv = take((size_t)T * OI_TILE * 8);
-      cd.P = ptiles(n) ? take((size_t)ptiles(n) * OI_TILE * 8) : nullptr;
       cd.vec = take(4 * (size_t)T * OI_NB * 8);
       cd.part = take((size_t)OI_PART_SIZE(nt, T) * 8);
       cd.xyt = job.sites + 3 * job.offs[c];
@@ -995,33 +908,13 @@ class Engine {
       const size_t idx = 2 * (gr.ev_kind.size() - 1) + (end ? 1 : 0);
       if (idx < gr.ev.size()) HIPC(hipEventRecord(gr.ev[idx], gst));
     };
-    static const double scale_fl = acct::scale_tile();
     int rc = 0;
     cur_cells = na;
     prep_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
     mark(K_BUILD, false);
     rc |= oi_launch_build(dc, dl_all, na, maxT, gst);
     mark(K_BUILD, true);
-    for (int j = 0; fold_ && j < maxT; j += 2) {  // folded pair step
-      int cnt = 0;
-      while (cnt < na && hc(all_slots[cnt]).T > j) ++cnt;
-      cur_j = j;
-      cur_cells = cnt;
-      mark(K_CHOL, false);
-      rc |= oi_launch_diag_pair(dc, dl_all, cnt, j, gst);
-      mark(K_CHOL, true);
-      // nothing below the block and no W rows (j = 0, or no fitting cell): no panel
-      if (j + 2 >= maxT && (j == 0 || ne == 0)) continue;
-      mark(K_PAIR, false);
-      rc |= oi_launch_panel_pair(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
-      mark(K_PAIR, true);
-      if (o_.profile)
-        for (int k = 0; k < cnt; ++k) {
-          const OiCell& cd = hc(all_slots[k]);
-          kfl_[K_PAIR] += acct::panel_pair(cd.T, cd.n, j, cd.mode == OI_MODE_EVAL);
-        }
-    }
-    for (int j = 0; !fold_ && j < maxT; ++j) {
+    for (int j = 0; j < maxT; ++j) {
       int cnt = 0;
       while (cnt < na && hc(all_slots[cnt]).T > j) ++cnt;
       cur_j = j;
@@ -1031,11 +924,6 @@ class Engine {
       mark(K_CHOL, true);
       const bool even = !legacy_ && (j % 2 == 0);
       const int kbeg = (legacy_ || even) ? 0 : j - 1;
-      if (pform_ && j > kbeg) {  // P_jk for kbeg <= k < j: nothing to scale at j = 0
-        mark(K_SCALE, false);
-        rc |= oi_launch_scale(dc, dl_all, cnt, j, kbeg, gst);
-        mark(K_SCALE, true);
-      }
       // the last column of a round with no fitting cell has neither factor
       // tiles below the diagonal nor a W row: its panel launch would be empty
       const bool empty_panel = j == maxT - 1 && ne == 0;
@@ -1046,23 +934,22 @@ class Engine {
         if (ke == K_EVEN4)
           rc |= oi_launch_panel4(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
         else
-          rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
+          rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
         mark(ke, true);
       } else {
         mark(K_TRSM, false);
-        rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, pform_ ? 1 : 0, gst);
+        rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, gst);
         mark(K_TRSM, true);
       }
       if (o_.profile) {  // executed MFMA flops, mirroring the kernels' masks (acct::)
         for (int k = 0; k < cnt; ++k) {
           const OiCell& cd = hc(all_slots[k]);
           const bool ev = cd.mode == OI_MODE_EVAL;
-          if (pform_ && j > kbeg) kfl_[K_SCALE] += scale_fl * (double)(j - kbeg);
           if (empty_panel) continue;
           const int kk = even ? (use_panel4(j, maxT) ? K_EVEN4 : K_EVEN) : K_TRSM;
           const double f = kk == K_EVEN4 ? acct::panel4(cd.T, cd.n, j, ev)
-                           : kk == K_EVEN ? acct::panel_even(cd.T, cd.n, j, ev, !pform_)
-                                          : acct::chol_panel(cd.T, cd.n, j, kbeg, ev, !pform_);
+                           : kk == K_EVEN ? acct::panel_even(cd.T, cd.n, j, ev, true)
+                                          : acct::chol_panel(cd.T, cd.n, j, kbeg, ev, true);
           kfl_[kk] += f;
           std::lock_guard<std::mutex> pl(g_prof_mu);
           g_byj[{kk, j}].flops += f;
@@ -1238,7 +1125,7 @@ class Engine {
 
   Context& ctx_;
   oi_options o_;
-  bool legacy_ = false, pform_ = false, poison_ = false, panel4_ = false, fold_ = false;
+  bool legacy_ = false, poison_ = false, panel4_ = false;
   int panel4_minj_ = 0, panel4_mint_ = 12;
   hipStream_t st_ = nullptr, ss_ = nullptr;
   hipEvent_t ready_ = nullptr;

@@ -186,20 +186,17 @@ def test_panel_schemes_agree(scheme, monkeypatch):
         assert abs(out[c, 1] - sd[0]) <= RTOL * max(1, abs(sd[0]))
 
 
-@pytest.mark.parametrize('knob,value', [('OI_DIAG', '32'), ('OI_DIAG', '16'), ('OI_LAUUM', '4'), ('OI_PFORM', '1'), ('OI_PANEL4', '0'),
-                                        ('OI_PANEL4_MINT', '0')])
+@pytest.mark.parametrize('knob,value', [('OI_PANEL4', '0'), ('OI_PANEL4_MINT', '0')])
 def test_alternate_kernels_agree(knob, value, monkeypatch):
-    """The A/B alternates kept in the library -- round 1's 32-blocked diagonal
-    factor (OI_DIAG=32; it also seeds alpha = W^T z and z = L^-1 r), round 2's
-    single-wave 16-blocked one (OI_DIAG=16; the default is the 4-wave kernel), the
-    128x128 K^-1 / gradient kernel (OI_LAUUM=4) and the P-form panels
-    (OI_PFORM=1: k_scale's P_jk = -Dinv_jj L_jk streamed by the panels, both
-    panel schemes) -- meet the T1 tolerance on tile-boundary sizes, fit and
-    predict."""
+    """The even-column panel core the engine selects per round -- k_panel_even
+    everywhere (OI_PANEL4=0) or k_panel4 in every round (OI_PANEL4_MINT=0; by
+    default only in rounds whose largest cell has >= 12 block columns) --
+    meets the T1 tolerance on tile-boundary sizes, fit and predict.  (Round 4
+    retired the other A/B alternates -- round 1's 32-blocked and round 2's
+    single-wave diagonal factors, the P-form panels with k_scale, the 128x128
+    K^-1 kernel and the folded pair step)"""
     monkeypatch.setenv(knob, value)
     test_panel_schemes_agree('2', monkeypatch)
-    if knob == 'OI_PFORM':
-        test_panel_schemes_agree('1', monkeypatch)
 
 
 def test_config5_size_n5000():
@@ -330,7 +327,6 @@ def test_panel4_equals_panel_even(monkeypatch):
     hyp = np.tile(synthetic.FIXED_HYPERS, (len(sizes), 1))
     res = {}
     monkeypatch.setenv('OI_PANEL4_MINT', '0')   # k_panel4 in every round (default: rounds with T >= 12)
-    monkeypatch.setenv('OI_FOLD', '0')          # the per-column scheme these panels belong to
     for p4 in ('0', '1'):
         for poison in ('0', '1'):
             monkeypatch.setenv('OI_PANEL4', p4)
@@ -343,47 +339,6 @@ def test_panel4_equals_panel_even(monkeypatch):
             assert np.array_equal(a, b), p4
     for a, b in zip(res[('1', '0')], res[('0', '0')]):
         assert np.all(np.abs(a - b) <= 1e-12 * np.maximum(1.0, np.abs(b))), np.max(np.abs(a - b) / np.maximum(1, np.abs(b)))
-
-
-def test_fold_equals_per_column(monkeypatch):
-    """The folded pair step (OI_FOLD=1, default: k_diag_pair factors and inverts
-    the 128 x 128 diagonal block, k_panel_pair finishes both block columns of a
-    row with Winv_JJ^T, no odd-column launch) against the per-column scheme
-    (k_diag_factor + k_panel4/k_panel_even + k_chol_panel): the same Cholesky,
-    rounded differently -- objective, gradient and predictions agree to 1e-10
-    relative on sizes around every tile boundary with T odd and even (the last
-    block column alone or in a pair), in eval and predict mode; poisoned
-    workspaces (OI_POISON=1) give bitwise the same results (nothing is read
-    before it is written, the scratch tiles in c.P included) and both schemes
-    match the oracle at the T1 tolerance."""
-    sizes = [1, 40, 64, 65, 127, 128, 129, 191, 192, 193, 255, 257, 320, 385, 700, 1100, 1500, 2000]
-    cells = synthetic.make_cells(sizes, seed=29)
-    h = np.tile(np.array([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(1e-3), 0.]), (len(sizes), 1))
-    mX = np.full(len(cells.z), cells.mean)
-    hyp = np.tile(synthetic.FIXED_HYPERS, (len(sizes), 1))
-    res = {}
-    for fold in ('0', '1'):
-        for poison in ('0', '1'):
-            monkeypatch.setenv('OI_FOLD', fold)
-            monkeypatch.setenv('OI_POISON', poison)
-            ev = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, h)
-            pr = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
-            res[(fold, poison)] = (ev[0], ev[1], pr[0][:, :3], ev[2], pr[1])
-    for fold in ('0', '1'):
-        for a, b in zip(res[(fold, '1')], res[(fold, '0')]):
-            assert np.array_equal(a, b), fold
-    f1, f0 = res[('1', '0')], res[('0', '0')]
-    assert np.array_equal(f1[3], f0[3]) and np.array_equal(f1[4], f0[4])  # status
-    for a, b in zip(f1[:3], f0[:3]):
-        err = np.abs(a - b) / np.maximum(1.0, np.abs(b))
-        assert np.all(err <= 1e-10), np.max(err)
-    # the folded scheme against the oracle (SMLII at the same hypers), small cells
-    for c, n in enumerate(sizes):
-        if n > 700:
-            continue
-        x, y = cells.xyt[cells.offs[c]:cells.offs[c + 1]], cells.z[cells.offs[c]:cells.offs[c + 1]]
-        f, g = O.neg_log_ml(h[c], x, y, mX[cells.offs[c]:cells.offs[c + 1]])
-        assert abs(f1[0][c] - f) <= 1e-10 * max(1.0, abs(f)), (n, f1[0][c], f)
 
 
 def test_profile_by_j_matches_kernel_totals():
