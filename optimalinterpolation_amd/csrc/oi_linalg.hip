@@ -342,10 +342,23 @@ __global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
         const double* col = A + (size_t)ld * c;
         const double vc = v[c];
         double dot = 0.0;
-        for (int r = c + lane; r < M; r += 64) {
-          const double a = col[r];
-          dot += a * v[r];
-          if (r > c) myw[r] += a * vc;
+        // 16 loads per lane in flight (the product streams M^3/6 doubles per
+        // matrix from L2 / MALL: memory-level parallelism, not arithmetic, sets its rate)
+        for (int r0 = c; r0 < M; r0 += 16 * 64) {
+          double a[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int r = r0 + lane + 64 * u;
+            a[u] = r < M ? col[r] : 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int r = r0 + lane + 64 * u;
+            if (r < M) {
+              dot += a[u] * v[r];
+              if (r > c) myw[r] += a[u] * vc;
+            }
+          }
         }
         for (int o = 32; o > 0; o >>= 1) dot += __shfl_down(dot, o, 64);
         if (lane == 0) myw[c] += dot;

@@ -167,3 +167,34 @@ def test_tiny_pool_nomem_then_normal_call():
         assert np.all(st == 0)
     ref, _, _ = _lib.gpr_batch(small.xyt, small.z, small.offs, small.xs, small.mean, opt=False, hyp=hyp)
     assert np.array_equal(got, ref)
+
+
+def test_session_unprofiled_groups_equal_profiled(monkeypatch):
+    """the unprofiled session completes rounds through the host flag
+    k_finalize writes into pinned memory (no stream synchronise), profiled
+    rounds synchronise instead.  With two stream groups (OI_GROUPS=2) and a
+    stream of small batches -- including batches whose cells are all n = 0 or
+    n = 1 (rounds with nothing to factor) -- both completion paths give the same
+    outputs, status and CG info bit for bit, and the round counter advances."""
+    monkeypatch.setenv('OI_GROUPS', '2')
+    rng = np.random.default_rng(77)
+    batches = []
+    for k in range(14):
+        if k in (3, 9):
+            sizes = [0, 0, 1]
+        else:
+            sizes = rng.integers(20, 260, int(rng.integers(1, 5)))
+        batches.append(synthetic.make_cells(sizes, seed=500 + k))
+    res = {}
+    for prof in (False, True):
+        _lib.profile_reset()
+        outs = []
+        with _lib.Session(profile=prof) as s:
+            t = [s.submit(b.xyt, b.z, b.offs, b.xs, b.mean, x0=X0) for b in batches]
+            for k, tk in enumerate(t):
+                outs.append(s.wait(tk))
+        res[prof] = outs
+        assert _lib.profile_json()['rounds'] > 0, prof
+    for a, b in zip(res[False], res[True]):
+        assert np.array_equal(a[0], b[0], equal_nan=True)
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])

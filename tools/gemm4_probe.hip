@@ -140,6 +140,101 @@ __global__ __launch_bounds__(512) void g4g(const double* A, const double* B, dou
   C[(size_t)blockIdx.x * 512 + t] = s;
 }
 
+
+// 256 x 128 output per 512-thread workgroup (one workgroup per CU): wave w owns
+// rows 64*(w>>1) .. +64 and columns 64*(w&1) .. +64 as 4 x 4 blocks (16 MFMAs
+// per 8 LDS reads); operands A = 4 tiles (rows), B = 2 tiles (columns).
+struct Acc16 { d4 c[4][4]; };
+template <bool GLDS, int NBUF>
+__global__ __launch_bounds__(512) void g8(const double* A, const double* B, double* C, int P, int mode) {
+  constexpr int ROW = 384, STG = KC * ROW;  // one k-row: A 256 | B 128
+  __shared__ __attribute__((aligned(16))) double lds[NBUF * STG];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  Acc16 acc;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc.c[a][b] = (d4){0, 0, 0, 0};
+  const int nch = P * 4;
+  // staging unit: 16 B pieces; chunk = 16 rows x 384 doubles = 3072 pieces = 6 per thread
+  // piece q of thread t: e = t + 512 q -> row k = e / 192, piece-in-row pr = e % 192 (tile pr / 32)
+  auto src = [&](int ch, int e) -> const double* {
+    const int p = ch >> 2, k0 = (ch & 3) * KC, k = e / 192, pr = e % 192, tl = pr >> 5;
+    const int sw = 8 * (k & 1);
+    const double* tp = tile(tl < 4 ? A : B, mode, blockIdx.x, P, p, tl < 4 ? tl : 2 + (tl - 4));
+    return tp + (k0 + k) * 64 + 2 * ((pr & 31) ^ sw);
+  };
+  // LDS image: row k, piece pr at k*ROW + 2*pr (linear); read index (m ^ 16 (k&1)) within each 64-tile
+  dv2 rg[2][6];
+  auto gload = [&](int ch, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) rg[slot][q] = gload2(src(ch, t + 512 * q));
+  };
+  auto sstore = [&](int buf, int slot) __attribute__((always_inline)) {
+    double* S = lds + buf * STG;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int e = t + 512 * q;
+      *(dv2*)(S + (e / 192) * ROW + 2 * (e % 192)) = rg[slot][q];
+    }
+  };
+  auto issue = [&](int ch, int buf) __attribute__((always_inline)) {
+    double* S = lds + buf * STG;
+    // 48 KB per chunk = 48 wave-instructions of 1 KB: 6 per wave; instruction i of wave w covers
+    // pieces (w*6 + i) * 64 .. +64 of the linear image
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int e0 = (w * 6 + i) * 64, e = e0 + lane;
+      __builtin_amdgcn_global_load_lds((const void*)src(ch, e), (void*)(S + 2 * e0 + 0 * lane), 16, 0, 0);
+    }
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const double* S = lds + buf * STG;
+#pragma unroll
+    for (int kk = 0; kk < KC / 4; ++kk) {
+      const int k = kk * 4 + fk, sw = 16 * (k & 1);
+      double a[4], b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = S[k * ROW + 64 * wr + ((16 * q + fr) ^ sw)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[q] = S[k * ROW + 256 + 64 * wc + ((16 * q + fr) ^ sw)];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc.c[x][y] = MFMA64(a[x], b[y], acc.c[x][y]);
+    }
+  };
+  if constexpr (!GLDS) {
+    gload(0, 0);
+    gload(min(1, nch - 1), 1);
+    sstore(0, 0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ch += 2) {
+      gload(min(ch + 2, nch - 1), 0);
+      compute(0);
+      sstore(1, 1);
+      __syncthreads();
+      gload(min(ch + 3, nch - 1), 1);
+      if (ch + 1 < nch) compute(1);
+      if (ch + 2 < nch) sstore(0, 0);
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < NBUF - 1; ++d) issue(min(d, nch - 1), d);
+    for (int ch = 0; ch < nch; ++ch) {
+      if constexpr (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue(min(ch + NBUF - 1, nch - 1), (ch + NBUF - 1) % NBUF);
+      compute(ch % NBUF);
+    }
+  }
+  double s = 0;
+  for (int a = 0; a < 4; ++a) for (int b = 0; b < 4; ++b) for (int q = 0; q < 4; ++q) s += acc.c[a][b][q];
+  C[(size_t)blockIdx.x * 512 + t] = s;
+}
+
 __global__ __launch_bounds__(512) void g2(const double* A, const double* B, double* C, int P, int mode) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
   Quad acc; quad_zero(acc);
@@ -202,6 +297,18 @@ int main() {
     chk("g4g kc16 nbuf2", g4g<16, 2>); chk("g4g kc16 nbuf3", g4g<16, 3>); chk("g4g kc8 nbuf4", g4g<8, 4>);
     chk("g4g kc8 nbuf3", g4g<8, 3>); chk("g4g kc32 nbuf2", g4g<32, 2>);
   }
+  {
+    auto res8 = [&](auto kern) {
+      std::vector<double> h((size_t)nwg / 2 * 512);
+      hipLaunchKernelGGL(kern, dim3(nwg / 2), dim3(512), 0, 0, A, B, C, P, 0); CHK(hipDeviceSynchronize());
+      CHK(hipMemcpy(h.data(), C, h.size() * 8, hipMemcpyDeviceToHost));
+      return h;
+    };
+    auto r0 = res8(g8<false, 2>), r1 = res8(g8<true, 2>), r2 = res8(g8<true, 3>);
+    size_t b1 = 0, b2 = 0;
+    for (size_t i = 0; i < r0.size(); ++i) { b1 += r1[i] != r0[i]; b2 += r2[i] != r0[i]; }
+    printf("check g8 glds2 %zu, glds3 %zu of %zu differ from g8 regs\n", b1, b2, r0.size());
+  }
   run("g1 64x64", g1, 256, 4 * nwg, tp);
   run("g2 64x128", g2, 512, 2 * nwg, 2 * tp);
   run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
@@ -212,5 +319,8 @@ int main() {
   run("g4g kc8 nbuf3", g4g<8, 3>, 512, nwg, 4 * tp);
   run("g4g kc32 nbuf2", g4g<32, 2>, 512, nwg, 4 * tp);
   run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
+  run("g8 256x128 regs", (g8<false, 2>), 512, nwg / 2, 8 * tp);
+  run("g8 256x128 glds2", (g8<true, 2>), 512, nwg / 2, 8 * tp);
+  run("g8 256x128 glds3", (g8<true, 3>), 512, nwg / 2, 8 * tp);
   return 0;
 }
