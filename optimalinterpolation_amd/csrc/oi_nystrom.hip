@@ -535,7 +535,7 @@ inline bool fused_objective() {
 struct Lane {
   hipStream_t st = nullptr;
   oila::Stager la;  // launch descriptors of the oila kernels on this lane's stream
-  Buf Knm, U1, ut, W, Ki, Wp, Av, tv, ks, kv, xsc, part;
+  Buf Knm, U1, ut, Ki, Wp, Av, tv, ks, kv, xsc, part;
   Stager sg;
   hipEvent_t done = nullptr;
   Lane(int64_t nmax, int64_t mmax, bool obj, bool pred, bool profile) {
@@ -546,7 +546,6 @@ struct Lane {
     Knm.alloc(nM * 8);
     U1.alloc(nM * 8);
     ut.alloc(nM * 8);
-    W.alloc(nM * 8);
     Av.alloc(nmax * 8);
     tv.alloc(mmax * 8);
     if (obj) {
@@ -795,6 +794,14 @@ class Runner {
                            stl_.as<double>() + s0 * mpmax_, mpmax_,
                            res_.as<double>() + g0 * NRES, (int64_t)NRES);
         KCHK();
+        // W' = C L^-T in place on each slot's C (n x M, leading dimension n): one
+        // batched right-looking block solve for the whole group
+        std::vector<oila::TrsmRLT> ts;
+        for (int q = 0; q < cnt; ++q) {
+          const CellRefs R = refs(g0 + q, s0 + q);
+          ts.push_back(oila::TrsmRLT{R.C, R.B, R.dinv, R.in, R.iM, R.in, R.iMp});
+        }
+        oila::trsm_right_lt(la_, st_, ts);
         sg_.end();
       }
       g0 = g1;
@@ -900,14 +907,11 @@ class Runner {
     hipStream_t st = L.st;
     const double sf2 = R.hp[3], isn2 = 1.0 / R.hp[4];
     const double dn = R.dn, dM = R.dM;
-    double* Wt = L.W.as<double>();  // n x M
+    double* Wt = R.C;  // n x M: W' = C L^-T, formed in place by batched()
     double* Av = L.Av.as<double>();
     double* tv = L.tv.as<double>();
     Stager& sg = L.sg;
     sg.begin(S_APPLY, 2.0 * dM * dM * dn + 4.0 * dn * dM, 16.0 * dn * dM);
-    // W' = C L^-T: copy C, then the right-looking block triangular solve
-    HC(hipMemcpyAsync(Wt, R.C, (size_t)R.n * R.M * 8, hipMemcpyDeviceToDevice, st));
-    oila::trsm_right_lt(L.la, st, {oila::TrsmRLT{Wt, R.B, R.dinv, R.in, R.iM, R.in, R.iMp}});
     hipLaunchKernelGGL(k_nys_vi, dim3(blocks(R.n, 256)), dim3(256), 0, st, R.r, R.n, isn2, Av);
     KCHK();
     oila::gemv(L.la, st, true, {oila::Gemv{Wt, R.r, tv, R.in, R.iM, R.in, 1.0, 0.0}});     // tv = W r

@@ -38,3 +38,22 @@ def test_pool_radius_covers_snapped_observations():
     d = np.hypot(x[:, 0] - 4e6, x[:, 1] - 4e6)
     assert d.max() <= synthetic.RADIUS_M + synthetic.GRID_M / np.sqrt(2) + 1e-6
     assert bench.POOL_PITCH_M > 2 * (synthetic.RADIUS_M + synthetic.GRID_M)
+
+
+def test_cpu_baseline_evaluations_come_from_the_reference_on_this_day():
+    """cpu_baseline's E(n): the reference's own evaluation
+    counts on the bench day's cells (tests/golden/day_ref_fits.npz, per 300-wide
+    n bucket), not a fit to other cells: every bucket value is the fixture's
+    own bucket mean over its cells and 5 observation orders, and the day-weighted
+    mean is their average."""
+    d = np.load('tests/golden/day_ref_fits.npz')
+    E, desc, e_fix = bench.reference_evals_model()
+    sizes, ev = d['sizes'], d['evals'].astype(float)
+    means = []
+    for lo in range(300, 3000, 300):
+        m = (sizes >= lo) & (sizes < (lo + 300 if lo < 2700 else 3001))
+        assert m.sum() >= 8
+        means.append(ev[m].mean())
+        assert np.allclose(E(np.array([lo, lo + 150, lo + 299])), ev[m].mean()), lo
+    assert abs(e_fix - np.mean(means)) < 1e-9 and 'day_ref_fits.npz' in desc
+    assert np.all(np.isfinite(E(np.array([3500.0, 5000.0]))))
