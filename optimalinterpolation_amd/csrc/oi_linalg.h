@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -100,6 +101,9 @@ void gemm(Stager& S, hipStream_t st, bool ta, bool tb, const std::vector<Gemm>& 
 void gemv(Stager& S, hipStream_t st, bool trans, const std::vector<Gemv>& g);
 void cholesky(Stager& S, hipStream_t st, const std::vector<Chol>& c);
 void trsm_right_lt(Stager& S, hipStream_t st, const std::vector<TrsmRLT>& t);
-void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& e);
+// mark(k), k = 0..4, is called between the phases (tridiagonalisation,
+// eigenpairs of the tridiagonal, orthogonalisation, back-transform, end)
+void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& e,
+          const std::function<void(int)>& mark = nullptr);
 
 }  // namespace oila

@@ -42,6 +42,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 
 #include "oi_gemm.h"
@@ -536,8 +537,39 @@ __global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ e
       if (cnt <= k) lo = mid;
       else hi = mid;
     }
-    const double lam = 0.5 * (lo + hi);
-    E.w[k] = lam;
+    E.w[k] = 0.5 * (lo + hi);
+  }
+  __syncthreads();
+  // The bottom cluster: eigenvalues 0 .. nb0-1 whose consecutive gaps are all
+  // <= 1e3 eps ||T|| -- the numerical null space of a rank-deficient K_mm
+  // (duplicated sites) and the noise band below it.  Inverse iteration cannot
+  // separate vectors whose eigenvalues differ by less than its own accuracy
+  // (they collapse onto the same few directions), so those vectors start
+  // from independent random vectors instead, and the orthogonalisation, which
+  // runs in DESCENDING eigenvalue order (eigenvector k is column M-1-k of Z
+  // until the final reversal), makes them an orthonormal basis of the
+  // complement of every other eigenvector -- the cluster's invariant subspace.
+  if (t == 0) {
+    const double gtol = 1e3 * eps * tnorm;
+    int nb0 = 1;
+    while (nb0 < M && E.w[nb0] - E.w[nb0 - 1] <= gtol) ++nb0;
+    red[4] = nb0 >= 2 ? (double)nb0 : 0.0;
+  }
+  __syncthreads();
+  const int nb0 = (int)red[4];
+  for (int k = t; k < M; k += blockDim.x) {
+    const double lam = E.w[k];
+    double* z = E.A + (size_t)E.lda * (M - 1 - k);
+    if (k < nb0) {
+      double nrm = 0.0;
+      for (int i = 0; i < M; ++i) {
+        const double x = start_value(k, i);
+        nrm += x * x;
+      }
+      const double inv = 1.0 / sqrt(nrm);
+      for (int i = 0; i < M; ++i) z[i] = start_value(k, i) * inv;
+      continue;
+    }
     // T - lam I = P L U (dlagtf), factors at [i * M + k]
     {
       double ak = d[0] - lam, bk = M > 1 ? ws.e[0] : 0.0;
@@ -619,8 +651,22 @@ __global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ e
       nrm += x * x;
     }
     const double inv = 1.0 / sqrt(nrm);
-    double* z = E.A + (size_t)E.lda * k;
     for (int i = 0; i < M; ++i) z[i] = sx[(size_t)i * M + k] * inv;
+  }
+}
+
+// column c <-> M-1-c (the eigenvectors back in ascending eigenvalue order)
+__global__ __launch_bounds__(256) void k_reverse_cols(const Eigh* __restrict__ es) {
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M;
+  for (int c = blockIdx.y; c < M / 2; c += gridDim.y) {
+    double* a = E.A + (size_t)E.lda * c;
+    double* b = E.A + (size_t)E.lda * (M - 1 - c);
+    for (int i = threadIdx.x; i < M; i += 256) {
+      const double x = a[i];
+      a[i] = b[i];
+      b[i] = x;
+    }
   }
 }
 
@@ -808,8 +854,11 @@ void trsm_right_lt(Stager& S, hipStream_t st, const std::vector<TrsmRLT>& ts) {
   }
 }
 
-void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es) {
+void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::function<void(int)>& mark) {
   if (es.empty()) return;
+  auto phase = [&](int k) {
+    if (mark) mark(k);
+  };
   int Mmax = 0;
   for (const Eigh& e : es) Mmax = std::max(Mmax, e.M);
   if (Mmax > 4096) throw LinalgErr{"eigh: M > 4096 not supported"};
@@ -817,10 +866,13 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es) {
   const unsigned n = (unsigned)es.size();
   const size_t lds_sy = ((size_t)(SY_W + 2) * Mmax + 64 + 2 * TNB + TNB * TNB) * sizeof(double);
   if (lds_sy > 160 * 1024) throw LinalgErr{"eigh: matrix too large for the tridiagonalisation's LDS"};
+  phase(0);
   hipLaunchKernelGGL(k_sytrd, dim3(n), dim3(SY_T), lds_sy, st, de);
   LC(hipGetLastError());
+  phase(1);
   hipLaunchKernelGGL(k_stebz_stein, dim3(n), dim3(1024), (2 * (size_t)Mmax + 64) * sizeof(double), st, de);
   LC(hipGetLastError());
+  phase(2);
   // BCGS2 over panels of TNB eigenvectors (columns of Z = E.A)
   for (int p = 0; p < Mmax; p += TNB) {
     if (p > 0) {
@@ -843,6 +895,7 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es) {
     LC(hipGetLastError());
   }
   // back-transform: Z <- (I - V_p T_p V_p') Z for the panels in reverse order
+  phase(3);
   const int npan = (Mmax - 1 + TNB - 1) / TNB;
   for (int pi = npan - 1; pi >= 0; --pi) {
     const int p = pi * TNB;
@@ -863,6 +916,9 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es) {
     gemm(S, st, false, false, g2);
     gemm(S, st, false, false, g3);
   }
+  hipLaunchKernelGGL(k_reverse_cols, dim3(n, 64), dim3(256), 0, st, de);
+  LC(hipGetLastError());
+  phase(4);
 }
 
 }  // namespace oila

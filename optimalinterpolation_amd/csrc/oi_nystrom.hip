@@ -346,9 +346,13 @@ struct HipErr {
 
 // opts.profile: HIP events around each stage of each cell, summed per stage
 // into oi_profile_json (algorithmic flops / bytes per stage alongside)
-enum { S_BUILD, S_EIGH, S_PANEL, S_KI, S_APPLY, S_LOGDET, S_GRAD, S_PRED, S_COUNT };
-const char* kStage[S_COUNT] = {"nys_build", "nys_eigh",   "nys_panels", "nys_ki_gemm",
-                               "nys_apply", "nys_logdet", "nys_grad",   "nys_predict"};
+enum { S_BUILD, S_EIGH, S_EIGH_VEC, S_EIGH_ORTH, S_EIGH_BACK, S_PANEL, S_KI, S_APPLY, S_LOGDET, S_GRAD,
+       S_PRED, S_COUNT };
+// nys_eigh = the Householder tridiagonalisation; the eigensolver's other phases
+// are timed as their own stages
+const char* kStage[S_COUNT] = {"nys_build",  "nys_eigh",   "nys_eigh_vectors", "nys_eigh_orth",
+                               "nys_eigh_back", "nys_panels", "nys_ki_gemm", "nys_apply",
+                               "nys_logdet", "nys_grad",   "nys_predict"};
 struct Stager {
   bool on = false;
   hipStream_t st = nullptr;
@@ -772,13 +776,19 @@ class Runner {
       const int64_t s0 = g0 - p0;
       const double dM = (double)M;
       if (which == 0) {
-        sg_.begin(S_EIGH, 4.0 * dM * dM * dM * cnt, 0.0);
         std::vector<oila::Eigh> es;
         for (int q = 0; q < cnt; ++q)
           es.push_back(oila::Eigh{Kmm_.as<double>() + (s0 + q) * mm, eval_.as<double>() + (s0 + q) * mpmax_,
                                   EW_.as<double>() + (s0 + q) * ewd_, iM, iM});
-        oila::eigh(la_, st_, es);
-        sg_.end();
+        // algorithmic flops per phase: tridiagonalisation 4/3 M^3, tridiagonal
+        // eigenpairs O(M^2), BCGS2 2 M^3, back-transform 2 M^3
+        const double m3 = dM * dM * dM * cnt;
+        const int kind[4] = {S_EIGH, S_EIGH_VEC, S_EIGH_ORTH, S_EIGH_BACK};
+        const double fl[4] = {4.0 / 3.0 * m3, 0.0, 2.0 * m3, 2.0 * m3};
+        oila::eigh(la_, st_, es, [&](int k) {
+          if (k > 0) sg_.end();
+          if (k < 4) sg_.begin(kind[k], fl[k], 0.0);
+        });
       } else {
         // L = chol(B); half log-determinants (the lanes then form W' = C L^-T
         // by a block triangular solve with the kept diagonal-block inverses)
