@@ -21,13 +21,17 @@
 //                 corrections, then the rank-2*32 trailing update per panel on
 //                 the MFMA core; V (unit lower, clean copy) and T (dlarft,
 //                 forward columnwise) kept per 32-column panel
-//   k_stebz_stein eigenvalues of the tridiagonal by bisection on Sturm counts
-//                 (dstebz), eigenvectors by inverse iteration with partial
-//                 pivoting (dlagtf / dlagts; dstein), one thread per
-//                 eigenvalue, pseudo-random start per eigenvalue
-//   k_mgs_panel   classical Gram-Schmidt twice inside a 32-vector panel, a
-//                 fresh start vector where one collapses (repeated
-//                 eigenvalues); between panels block Gram-Schmidt twice
+//   k_stebz       eigenvalues of the tridiagonal by bisection on Sturm counts
+//                 (dstebz), one thread per eigenvalue
+//   k_stein       eigenvectors by inverse iteration with partial pivoting
+//                 (dlagtf / dlagts; dstein), one thread per eigenvalue,
+//                 pseudo-random start per eigenvalue; k_stein_out transposes
+//                 them into Z
+//   k_orth_panel  Cholesky QR twice inside a 32-vector panel (Gram-Schmidt
+//                 in column order; G = Z'Z on MFMA); where a column
+//                 collapses (repeated eigenvalues) classical Gram-Schmidt
+//                 twice column by column with fresh start vectors
+//                 (k_mgs_panel); between panels block Gram-Schmidt twice
 //                 (BCGS2) on k_gemm
 //   back-transform U = Q Z, one block reflector I - V T V' per panel (k_gemm)
 // The algorithm is modelled step for step in tools/eigh_model.py.
@@ -227,9 +231,11 @@ __global__ __launch_bounds__(64) void k_potrf_tile(const Chol* __restrict__ cs, 
 #define TNB 32   // panel width
 #define SY_T 512 // threads
 #define SY_W (SY_T / 64)
+#define SY_C 8   // symv: columns per wave group
+#define SY_R 8   // symv: 64-row chunks per load batch
 
 struct EighWs {  // per-matrix workspace carve-up (eigh_workspace_doubles)
-  double *Vc, *Ws, *T, *d, *e, *tau, *scr, *H, *X, *Y;
+  double *Vc, *Ws, *T, *d, *e, *tau, *scr, *H, *X, *Y, *flag;
 };
 __host__ __device__ inline EighWs carve(double* w, int M) {
   EighWs s;
@@ -244,6 +250,7 @@ __host__ __device__ inline EighWs carve(double* w, int M) {
   s.d = s.T + ((size_t)(M + TNB - 1) / TNB + 1) * TNB * TNB;
   s.e = s.d + M + 1;
   s.tau = s.e + M + 1;
+  s.flag = s.tau + M + 1;  // k_orth_panel -> k_mgs_panel: the panel collapsed
   return s;
 }
 size_t eigh_workspace_doubles(int M) {
@@ -272,11 +279,36 @@ __device__ __forceinline__ void wg_sum(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
-// dynamic LDS: yw[SY_W][M] | v[M] | y[M] | red[64] | pan[2 * TNB] | G[TNB * TNB]
-__global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
+// phase cycle counts of matrix 0 (tools/eigh_probe.cpp builds with OI_SYTRD_TIMING)
+#ifdef OI_SYTRD_TIMING
+__device__ unsigned long long g_sy_cycles[8];
+#define SY_STAMP(k)                                                        \
+  do {                                                                     \
+    __syncthreads();                                                       \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                             \
+      const unsigned long long now_ = clock64();                           \
+      g_sy_cycles[k] += now_ - sy_last_;                                   \
+      sy_last_ = now_;                                                     \
+    }                                                                      \
+  } while (0)
+extern "C" int oila_sytrd_cycles(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sy_cycles), sizeof(g_sy_cycles)) == hipSuccess ? 0 : -1;
+}
+#else
+#define SY_STAMP(k) do {} while (0)
+#endif
+// dynamic LDS: yw[SY_W][M] | v[M] | y[M] | red[64] | pan[2 * TNB] | Tl[TNB * TNB]
+__device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] = E.A[0]; }
+// Panel p (columns p .. p+nb-1) of the tridiagonalisation, one workgroup per
+// matrix; the panel's trailing update runs after it on oila::gemm.
+__global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ es, int p) {
   extern __shared__ double sm[];
   const Eigh E = es[blockIdx.x];
   const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (p >= M - 1) {
+    if (p == 0 && t == 0) ws_d0(E);  // M == 1
+    return;
+  }
   double* A = E.A;
   EighWs ws = carve(E.work, M);
   double* yw = sm;
@@ -284,11 +316,14 @@ __global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
   double* y = v + M;
   double* red = y + M;
   double* pan = red + 64;  // pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v
-  double* G = pan + 2 * TNB; // TNB x TNB Gram of a panel's V (dlarft)
+  double* Tl = pan + 2 * TNB; // TNB x TNB: T of the current panel's block reflector
   for (int i = t; i < SY_W * M; i += SY_T) yw[i] = 0.0;
-  if (M == 1 && t == 0) ws.d[0] = A[0];
+  for (int i = t; i < TNB * TNB; i += SY_T) Tl[i] = 0.0;
   __syncthreads();
-  for (int p = 0; p < M - 1; p += TNB) {
+#ifdef OI_SYTRD_TIMING
+  unsigned long long sy_last_ = clock64();
+#endif
+  {
     const int nb = min(TNB, M - 1 - p);
     for (int i = 0; i < nb; ++i) {
       const int g = p + i;
@@ -296,6 +331,7 @@ __global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
       if (i > 0) {
         for (int r = g + t; r < M; r += SY_T) {
           double s = A[r + (size_t)ld * g];
+#pragma unroll 16
           for (int q = 0; q < i; ++q) {
             const double* vq = ws.Vc + (size_t)M * (p + q);
             const double* wq = ws.Ws + (size_t)M * q;
@@ -305,6 +341,7 @@ __global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
         }
         __syncthreads();
       }
+      SY_STAMP(0);
       // (2) reflector annihilating A(g+2:M, g) (dlarfg)
       double xs[1] = {0.0};
       for (int r = g + 2 + t; r < M; r += SY_T) {
@@ -336,44 +373,104 @@ __global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
         ws.tau[g] = tau;
       }
       __syncthreads();
-      // (3) y = A22 v over the lower triangle of A(g+1:M, g+1:M): wave wv owns
-      // columns c = g+1+wv, +SY_W, ...; the transposed half goes to yw[wv][r]
+      SY_STAMP(1);
+      // (3) y = A22 v over the lower triangle of A(g+1:M, g+1:M).  Wave wv owns
+      // groups of SY_C consecutive columns (c0 = g+1 + SY_C (wv + SY_W j)) and
+      // streams their rows in batches of SY_R x 64, so SY_C x SY_R loads per lane
+      // are in flight (one workgroup per matrix: load latency, not bandwidth,
+      // bounds the symv); per row one v[r] read and one yw[wv][r]
+      // read-modify-write (the transposed half) serve the whole group, and the
+      // group's column dots are reduced once at its end
       double* myw = yw + (size_t)wv * M;
-      for (int c = g + 1 + wv; c < M; c += SY_W) {
-        const double* col = A + (size_t)ld * c;
-        const double vc = v[c];
-        double dot = 0.0;
-        // 16 loads per lane in flight (the product streams M^3/6 doubles per
-        // matrix from L2 / MALL: memory-level parallelism, not arithmetic, sets its rate)
-        for (int r0 = c; r0 < M; r0 += 16 * 64) {
-          double a[16];
+      for (int c0 = g + 1 + SY_C * wv; c0 < M; c0 += SY_C * SY_W) {
+        const double* col = A + (size_t)ld * c0;
+        double vc[SY_C], dot[SY_C];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int r = r0 + lane + 64 * u;
-            a[u] = r < M ? col[r] : 0.0;
-          }
+        for (int j = 0; j < SY_C; ++j) {
+          vc[j] = c0 + j < M ? v[c0 + j] : 0.0;
+          dot[j] = 0.0;
+        }
+        for (int r0 = c0; r0 < M; r0 += SY_R * 64) {
+          double a[SY_R][SY_C];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
+          for (int u = 0; u < SY_R; ++u)
+#pragma unroll
+            for (int j = 0; j < SY_C; ++j) {
+              const int r = r0 + lane + 64 * u;
+              a[u][j] = (r < M && r >= c0 + j) ? col[r + (size_t)ld * j] : 0.0;
+            }
+#pragma unroll
+          for (int u = 0; u < SY_R; ++u) {
             const int r = r0 + lane + 64 * u;
             if (r < M) {
-              dot += a[u] * v[r];
-              if (r > c) myw[r] += a[u] * vc;
+              const double vr = v[r];
+              double tr = 0.0;
+#pragma unroll
+              for (int j = 0; j < SY_C; ++j) {
+                dot[j] += a[u][j] * vr;
+                if (r > c0 + j) tr += a[u][j] * vc[j];
+              }
+              myw[r] += tr;
             }
           }
         }
-        for (int o = 32; o > 0; o >>= 1) dot += __shfl_down(dot, o, 64);
-        if (lane == 0) myw[c] += dot;
+#pragma unroll
+        for (int j = 0; j < SY_C; ++j)
+          for (int o = 32; o > 0; o >>= 1) dot[j] += __shfl_down(dot[j], o, 64);
+        if (lane == 0)
+#pragma unroll
+          for (int j = 0; j < SY_C; ++j)
+            if (c0 + j < M) myw[c0 + j] += dot[j];
       }
+      SY_STAMP(2);
       // panel corrections: pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g)
-      for (int jq = wv; jq < 2 * i; jq += SY_W) {
-        const int q = jq % i;
-        const double* col = jq < i ? ws.Ws + (size_t)M * q : ws.Vc + (size_t)M * (p + q);
-        double s = 0.0;
-        for (int r = g + 1 + lane; r < M; r += 64) s += col[r] * v[r];
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-        if (lane == 0) pan[(jq < i ? 0 : TNB) + q] = s;
+      // (4 dots per wave at a time, 4 row chunks each: 16 loads per lane in flight)
+      for (int jq0 = 4 * wv; jq0 < 2 * i; jq0 += 4 * SY_W) {
+        const double* col[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int jq = min(jq0 + d, 2 * i - 1), q = jq % i;
+          col[d] = jq < i ? ws.Ws + (size_t)M * q : ws.Vc + (size_t)M * (p + q);
+        }
+        double s4[4][4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) s4[d][u] = 0.0;
+        for (int r = g + 1 + lane; r < M; r += 256) {
+          double a[4][4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) a[d][u] = r + 64 * u < M ? col[d][r + 64 * u] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const double vr = r + 64 * u < M ? v[r + 64 * u] : 0.0;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) s4[d][u] += a[d][u] * vr;
+          }
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          double s = (s4[d][0] + s4[d][1]) + (s4[d][2] + s4[d][3]);
+          for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+          const int jq = jq0 + d;
+          if (lane == 0 && jq < 2 * i) pan[(jq < i ? 0 : TNB) + jq % i] = s;
+        }
       }
       __syncthreads();
+      SY_STAMP(3);
+      // column i of the block reflector's T (dlarft, forward columnwise):
+      // T(i,i) = tau, T(a,i) = -tau sum_{a<=k<i} T(a,k) (V_k'v), V_k'v = pan[TNB + k]
+      if (t <= i) {
+        double x = tau;
+        if (t < i) {
+          x = 0.0;
+          for (int k = t; k < i; ++k) x += Tl[t + TNB * k] * pan[TNB + k];
+          x *= -tau;
+        }
+        Tl[t + TNB * i] = x;
+      }
       // (4) w = tau (y - V (W'v) - W (V'v)), then w += -tau/2 (w'v) v
       double sv[1] = {0.0};
       for (int r = g + 1 + t; r < M; r += SY_T) {
@@ -383,6 +480,7 @@ __global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
           s += yw[(size_t)ww * M + r];
           yw[(size_t)ww * M + r] = 0.0;
         }
+#pragma unroll 16
         for (int q = 0; q < i; ++q)
           s -= ws.Vc[(size_t)M * (p + q) + r] * pan[q] + ws.Ws[(size_t)M * q + r] * pan[TNB + q];
         const double wr = tau * s;
@@ -395,82 +493,25 @@ __global__ __launch_bounds__(SY_T) void k_sytrd(const Eigh* __restrict__ es) {
       for (int r = t; r < M; r += SY_T) wcol[r] = r <= g ? 0.0 : y[r] + a2 * v[r];
       __syncthreads();
     }
-    // T of the block reflector H_p ... H_{p+nb-1} = I - V T V' (dlarft, forward
-    // columnwise): T(i,i) = tau_i, T(0:i, i) = -tau_i T(0:i, 0:i) (V(:, 0:i)' v_i)
+    SY_STAMP(4);
+    // T of the block reflector H_p ... H_{p+nb-1} = I - V T V' (formed column
+    // by column in step (4)) to the workspace for the back-transform
     double* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
-    for (int jq = wv; jq < nb * nb; jq += SY_W) {
-      const int a = jq % nb, b = jq / nb;
-      if (a >= b) continue;
-      const double* va = ws.Vc + (size_t)M * (p + a);
-      const double* vb = ws.Vc + (size_t)M * (p + b);
-      double s = 0.0;
-      for (int r = p + b + 1 + lane; r < M; r += 64) s += va[r] * vb[r];
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-      if (lane == 0) G[a * TNB + b] = s;
+    for (int e = t; e < TNB * TNB; e += SY_T) {
+      Tp[e] = Tl[e];
+      Tl[e] = 0.0;
     }
-    __syncthreads();
-    if (t == 0) {
-      for (int b = 0; b < TNB; ++b)
-        for (int a = 0; a < TNB; ++a) Tp[a + TNB * b] = 0.0;
-      for (int b = 0; b < nb; ++b) {
-        const double tb = ws.tau[p + b];
-        Tp[b + TNB * b] = tb;
-        for (int a = 0; a < b; ++a) {
-          double s = 0.0;
-          for (int k = a; k < b; ++k) s += Tp[a + TNB * k] * G[k * TNB + b];
-          Tp[a + TNB * b] = -tb * s;
-        }
-      }
-    }
-    __syncthreads();
-    // trailing update A(q0:M, q0:M) -= V W' + W V' (lower triangle), 32 x 32
-    // quadrants of the MFMA core, operands [V | W] (rows) x [W | V] (columns)
-    const int q0 = p + nb, L = M - q0;
-    if (L > 0) {
-      const int nq = (L + 31) / 32;
-      const int fr = lane & 15, fk = lane >> 4;
-      for (int task = wv; task < nq * nq; task += SY_W) {
-        const int bi = task % nq, bj = task / nq;
-        if (bi < bj) continue;
-        const int r0 = q0 + 32 * bi, c0 = q0 + 32 * bj;
-        Quad acc;
-        quad_zero(acc);
-        for (int kk = 0; kk < 2 * TNB / 4; ++kk) {
-          const int k = 4 * kk + fk, q = k % TNB;
-          const bool first = k < TNB;  // k < 32: V(r) W(c)', else W(r) V(c)'
-          const double* Ar = first ? ws.Vc + (size_t)M * (p + q) : ws.Ws + (size_t)M * q;
-          const double* Bc = first ? ws.Ws + (size_t)M * q : ws.Vc + (size_t)M * (p + q);
-          const bool live = q < nb;
-          double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-          if (live) {
-            const int ra = r0 + fr, rb = r0 + 16 + fr, ca = c0 + fr, cb = c0 + 16 + fr;
-            a0 = ra < M ? Ar[ra] : 0.0;
-            a1 = rb < M ? Ar[rb] : 0.0;
-            b0 = ca < M ? Bc[ca] : 0.0;
-            b1 = cb < M ? Bc[cb] : 0.0;
-          }
-          acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
-          acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
-          acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
-          acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
-        }
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-          for (int nbk = 0; nbk < 2; ++nbk)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              const int r = r0 + 16 * mb + (lane >> 4) + 4 * rr, c = c0 + 16 * nbk + (lane & 15);
-              if (r < M && c < M && r >= c) A[r + (size_t)ld * c] -= acc.c[mb][nbk][rr];
-            }
-      }
-    }
-    __syncthreads();
+    SY_STAMP(5);
   }
-  if (t == 0 && M > 1) ws.d[M - 1] = A[(M - 1) + (size_t)ld * (M - 1)];
 }
 
-// ------------------------------------------------------------ k_stebz_stein
+// d[M-1] once the last panel's trailing update has run
+__global__ __launch_bounds__(64) void k_sytrd_last(const Eigh* __restrict__ es) {
+  const Eigh E = es[blockIdx.x];
+  if (threadIdx.x == 0 && E.M > 1) carve(E.work, E.M).d[E.M - 1] = E.A[(E.M - 1) + (size_t)E.lda * (E.M - 1)];
+}
+
+// ------------------------------------------------- k_stebz / k_stein
 __device__ __forceinline__ double start_value(int k, int i) {
   // deterministic pseudo-random start (splitmix64 of (k, i)) in [-1, 1)
   unsigned long long h = (unsigned long long)i * 0x9E3779B97F4A7C15ull + (unsigned long long)(k + 1) * 0xBF58476D1CE4E5B9ull;
@@ -480,16 +521,14 @@ __device__ __forceinline__ double start_value(int k, int i) {
   return (double)(h >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
 }
 
+// Eigenpairs of the tridiagonal, ST_T eigenvalues per workgroup (grid
+// matrices x ceil(M / ST_T)): the bisections and inverse iterations are long
+// serial chains per thread, so the batch is spread over the whole chip.
 // dynamic LDS: d[M] | e2[M] | red[64]
-__global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ es) {
-  extern __shared__ double sm[];
-  const Eigh E = es[blockIdx.x];
+#define ST_T 64
+__device__ __forceinline__ void tri_setup(const Eigh& E, const EighWs& ws, double* d, double* e2, double* red) {
   const int M = E.M, t = threadIdx.x;
-  EighWs ws = carve(E.work, M);
-  double* d = sm;
-  double* e2 = d + M;
-  double* red = e2 + M;
-  for (int i = t; i < M; i += blockDim.x) {
+  for (int i = t; i < M; i += ST_T) {
     d[i] = ws.d[i];
     e2[i] = i < M - 1 ? ws.e[i] * ws.e[i] : 0.0;
   }
@@ -510,16 +549,23 @@ __global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ e
     red[3] = pivmin;
   }
   __syncthreads();
-  const double GL = red[0], GU = red[1], tnorm = red[2], pivmin = red[3];
+}
+
+__global__ __launch_bounds__(ST_T) void k_stebz(const Eigh* __restrict__ es) {
+  extern __shared__ double sm[];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M, t = threadIdx.x;
+  if ((int)blockIdx.y * ST_T >= M) return;
+  EighWs ws = carve(E.work, M);
+  double* d = sm;
+  double* e2 = d + M;
+  double* red = e2 + M;
+  tri_setup(E, ws, d, e2, red);
+  const double GL = red[0], GU = red[1], pivmin = red[3];
   const double eps = 2.220446049250313e-16;
-  const size_t MM = (size_t)M * M;
-  double* sa = ws.scr;          // U diagonal
-  double* sb = sa + MM;         // U first superdiagonal
-  double* sc = sb + MM;         // U second superdiagonal
-  double* sl = sc + MM;         // L multipliers
-  double* sp = sl + MM;         // row interchange flags
-  double* sx = sp + MM;         // iterate
-  for (int k = t; k < M; k += blockDim.x) {
+  {
+    const int k = (int)blockIdx.y * ST_T + t;
+    if (k >= M) return;
     // eigenvalue k (ascending): count(x) = #eigenvalues < x; lambda_k = sup{x : count(x) <= k}
     double lo = GL, hi = GU;
     for (int it = 0; it < 128; ++it) {
@@ -539,7 +585,29 @@ __global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ e
     }
     E.w[k] = 0.5 * (lo + hi);
   }
-  __syncthreads();
+}
+
+// eigenvector k of the tridiagonal into the stein iterate (element i at
+// [i M + k], lanes over k: coalesced), its inverse norm into Ws[k]
+__global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
+  extern __shared__ double sm[];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M, t = threadIdx.x;
+  if ((int)blockIdx.y * ST_T >= M) return;
+  EighWs ws = carve(E.work, M);
+  double* d = sm;
+  double* e2 = d + M;
+  double* red = e2 + M;
+  tri_setup(E, ws, d, e2, red);
+  const double tnorm = red[2];
+  const double eps = 2.220446049250313e-16;
+  const size_t MM = (size_t)M * M;
+  double* sa = ws.scr;          // U diagonal
+  double* sb = sa + MM;         // U first superdiagonal
+  double* sc = sb + MM;         // U second superdiagonal
+  double* sl = sc + MM;         // L multipliers
+  double* sp = sl + MM;         // row interchange flags
+  double* sx = sp + MM;         // iterate
   // The bottom cluster: eigenvalues 0 .. nb0-1 whose consecutive gaps are all
   // <= 1e3 eps ||T|| -- the numerical null space of a rank-deficient K_mm
   // (duplicated sites) and the noise band below it.  Inverse iteration cannot
@@ -557,18 +625,19 @@ __global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ e
   }
   __syncthreads();
   const int nb0 = (int)red[4];
-  for (int k = t; k < M; k += blockDim.x) {
+  {
+    const int k = (int)blockIdx.y * ST_T + t;
+    if (k >= M) return;
     const double lam = E.w[k];
-    double* z = E.A + (size_t)E.lda * (M - 1 - k);
     if (k < nb0) {
       double nrm = 0.0;
       for (int i = 0; i < M; ++i) {
         const double x = start_value(k, i);
         nrm += x * x;
       }
-      const double inv = 1.0 / sqrt(nrm);
-      for (int i = 0; i < M; ++i) z[i] = start_value(k, i) * inv;
-      continue;
+      for (int i = 0; i < M; ++i) sx[(size_t)i * M + k] = start_value(k, i);
+      ws.Ws[k] = 1.0 / sqrt(nrm);
+      return;
     }
     // T - lam I = P L U (dlagtf), factors at [i * M + k]
     {
@@ -650,8 +719,28 @@ __global__ __launch_bounds__(1024) void k_stebz_stein(const Eigh* __restrict__ e
       const double x = sx[(size_t)i * M + k];
       nrm += x * x;
     }
-    const double inv = 1.0 / sqrt(nrm);
-    for (int i = 0; i < M; ++i) z[i] = sx[(size_t)i * M + k] * inv;
+    ws.Ws[k] = 1.0 / sqrt(nrm);
+  }
+}
+
+
+// Z(:, M-1-k) = iterate k * Ws[k]: the iterate transposed through 64 x 64 LDS tiles
+__global__ __launch_bounds__(256) void k_stein_out(const Eigh* __restrict__ es) {
+  __shared__ double tile[64][65];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M, nt = (M + 63) / 64;
+  if ((int)blockIdx.y >= nt * nt) return;
+  const EighWs ws = carve(E.work, M);
+  const double* sx = ws.scr + 5 * (size_t)M * M;
+  const int i0 = 64 * ((int)blockIdx.y % nt), k0 = 64 * ((int)blockIdx.y / nt), t = threadIdx.x;
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int i = i0 + e / 64, k = k0 + e % 64;
+    tile[e / 64][e % 64] = (i < M && k < M) ? sx[(size_t)i * M + k] * ws.Ws[k] : 0.0;
+  }
+  __syncthreads();
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int i = i0 + e % 64, k = k0 + e / 64;
+    if (i < M && k < M) E.A[i + (size_t)E.lda * (M - 1 - k)] = tile[e % 64][e / 64];
   }
 }
 
@@ -680,7 +769,7 @@ __global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es,
   __shared__ double red[4 * 33];
   const Eigh E = es[blockIdx.x];
   const int M = E.M;
-  if (p >= M) return;
+  if (p >= M || carve(E.work, M).flag[0] == 0.0) return;  // k_orth_panel's Cholesky QR held
   const int q = min(M, p + TNB), t = threadIdx.x, lane = t & 63, w = t >> 6;
   double* Z = E.A;
   const size_t ld = E.lda;
@@ -743,6 +832,136 @@ __global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es,
       for (int i = t; i < M; i += MG_T) zj[i] = start_value(j + 7919 * (attempt + 1), i);
       __syncthreads();
     }
+  }
+}
+
+
+// Columns [p, q) of Z (already orthogonal to columns < p): Cholesky QR twice --
+// G = Z_p' Z_p on the MFMA core, G = R'R, Z_p <- Z_p R^-1 -- the same
+// Gram-Schmidt in column order as mgs_panel in 2 block reductions per pass
+// instead of 4 per column.  A pivot that keeps no more than 1e-4 of its
+// column's squared norm (mgs_panel's collapse rule: numerically repeated
+// eigenvalues) hands the panel to k_mgs_panel and its fresh start vectors.
+#define RL (TNB + 1)  // LDS row stride of R and R^-1
+__global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es, int p) {
+  __shared__ double Gw[MG_T / 64][TNB * TNB];
+  __shared__ double R[TNB * RL];
+  __shared__ double Ri[TNB * RL];
+  __shared__ double gd[TNB];
+  __shared__ int bad;
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M;
+  if (p >= M) return;
+  const int nb = min(TNB, M - p), t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const size_t ld = E.lda;
+  double* Z = E.A + ld * p;
+  if (t == 0) carve(E.work, M).flag[0] = 0.0;
+  for (int pass = 0; pass < 2; ++pass) {
+    // (1) G = Z_p' Z_p: wave w sums the 16-row blocks 16 (w + 4 j), 4 k-steps per batch
+    Quad acc;
+    quad_zero(acc);
+    for (int i0 = 16 * w; i0 < M; i0 += 16 * (MG_T / 64)) {
+      double a0[4], a1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 4 * u + fk;
+        a0[u] = (i < M && fr < nb) ? Z[i + ld * fr] : 0.0;
+        a1[u] = (i < M && 16 + fr < nb) ? Z[i + ld * (16 + fr)] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.c[0][0] = MFMA64(a0[u], a0[u], acc.c[0][0]);
+        acc.c[0][1] = MFMA64(a0[u], a1[u], acc.c[0][1]);
+        acc.c[1][0] = MFMA64(a1[u], a0[u], acc.c[1][0]);
+        acc.c[1][1] = MFMA64(a1[u], a1[u], acc.c[1][1]);
+      }
+    }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nbk = 0; nbk < 2; ++nbk)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          Gw[w][(16 * mb + (lane >> 4) + 4 * rr) + TNB * (16 * nbk + (lane & 15))] = acc.c[mb][nbk][rr];
+    if (t == 0) bad = 0;
+    __syncthreads();
+    for (int e = t; e < TNB * TNB; e += MG_T) {
+      const int a = e % TNB, b = e / TNB;
+      double g = 0.0;
+      if (a <= b && b < nb) {
+        g = Gw[0][e];
+        for (int ww = 1; ww < MG_T / 64; ++ww) g += Gw[ww][e];
+      }
+      R[a + RL * b] = g;
+      if (a == b) gd[a] = g;
+    }
+    __syncthreads();
+    // (2) G = R'R (upper R, right-looking, row j scaled by its pivot)
+    for (int j = 0; j < nb; ++j) {
+      if (t == 0) {
+        const double dj = R[j + RL * j];
+        if (!(dj > 1e-4 * gd[j])) bad = 1;
+        R[j + RL * j] = sqrt(fmax(dj, 1e-300));
+      }
+      __syncthreads();
+      const double inv = 1.0 / R[j + RL * j];
+      for (int l = j + 1 + t; l < nb; l += MG_T) R[j + RL * l] *= inv;
+      __syncthreads();
+      const int L = nb - j - 1;
+      for (int e = t; e < L * L; e += MG_T) {
+        const int a = j + 1 + e % L, b = j + 1 + e / L;
+        if (a <= b) R[a + RL * b] -= R[j + RL * a] * R[j + RL * b];
+      }
+      __syncthreads();
+    }
+    if (bad) {  // k_mgs_panel takes the panel over
+      if (t == 0) carve(E.work, M).flag[0] = 1.0;
+      return;
+    }
+    // (3) R^-1 (upper), one thread per column
+    if (t < TNB) {
+      const int l = t;
+      for (int a = TNB - 1; a >= 0; --a) {
+        double x = 0.0;
+        if (l < nb && a <= l) {
+          x = a == l ? 1.0 : 0.0;
+          for (int k = a + 1; k <= l; ++k) x -= R[a + RL * k] * Ri[k + RL * l];
+          x /= R[a + RL * a];
+        }
+        Ri[a + RL * l] = x;
+      }
+    }
+    __syncthreads();
+    // (4) Z_p <- Z_p R^-1 on the MFMA core, wave w over the 16-row blocks 16 (w + 4 j)
+    double rb[2][TNB / 4];
+#pragma unroll
+    for (int kk = 0; kk < TNB / 4; ++kk)
+#pragma unroll
+      for (int nbk = 0; nbk < 2; ++nbk) rb[nbk][kk] = Ri[(4 * kk + fk) + RL * (16 * nbk + fr)];
+    for (int i0 = 16 * w; i0 < M; i0 += 16 * (MG_T / 64)) {
+      double za[TNB / 4];
+#pragma unroll
+      for (int kk = 0; kk < TNB / 4; ++kk) {
+        const int i = i0 + fr, a = 4 * kk + fk;
+        za[kk] = (i < M && a < nb) ? Z[i + ld * a] : 0.0;
+      }
+      d4 o0 = (d4){0.0, 0.0, 0.0, 0.0}, o1 = o0;
+#pragma unroll
+      for (int kk = 0; kk < TNB / 4; ++kk) {
+        o0 = MFMA64(za[kk], rb[0][kk], o0);
+        o1 = MFMA64(za[kk], rb[1][kk], o1);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = i0 + (lane >> 4) + 4 * rr, c = lane & 15;
+        if (i < M) {
+          if (c < nb) Z[i + ld * c] = o0[rr];
+          if (16 + c < nb) Z[i + ld * (16 + c)] = o1[rr];
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -867,10 +1086,36 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   const size_t lds_sy = ((size_t)(SY_W + 2) * Mmax + 64 + 2 * TNB + TNB * TNB) * sizeof(double);
   if (lds_sy > 160 * 1024) throw LinalgErr{"eigh: matrix too large for the tridiagonalisation's LDS"};
   phase(0);
-  hipLaunchKernelGGL(k_sytrd, dim3(n), dim3(SY_T), lds_sy, st, de);
+  // panel by panel: the panel's 32 reflectors on one workgroup per matrix,
+  // then its trailing update A22 -= V W' + W V' (lower 64 x 64 tiles) as two
+  // batched GEMMs over the whole chip
+  for (int p = 0; p < std::max(Mmax - 1, 1); p += TNB) {
+    hipLaunchKernelGGL(k_sytrd_panel, dim3(n), dim3(SY_T), lds_sy, st, de, p);
+    LC(hipGetLastError());
+    std::vector<Gemm> g1, g2;
+    for (const Eigh& e : es) {
+      const int nb = std::min(TNB, e.M - 1 - p), q0 = p + nb, L = e.M - q0;
+      if (nb <= 0 || L <= 0) continue;
+      EighWs w = carve(e.work, e.M);
+      double* C = e.A + q0 + (size_t)e.lda * q0;
+      const double* V = w.Vc + (size_t)e.M * p + q0;
+      const double* W = w.Ws + q0;
+      g1.push_back(Gemm{V, W, C, L, L, nb, e.M, e.M, e.lda, -1.0, 1.0, 1});
+      g2.push_back(Gemm{W, V, C, L, L, nb, e.M, e.M, e.lda, -1.0, 1.0, 1});
+    }
+    gemm(S, st, false, true, g1);
+    gemm(S, st, false, true, g2);
+  }
+  hipLaunchKernelGGL(k_sytrd_last, dim3(n), dim3(64), 0, st, de);
   LC(hipGetLastError());
   phase(1);
-  hipLaunchKernelGGL(k_stebz_stein, dim3(n), dim3(1024), (2 * (size_t)Mmax + 64) * sizeof(double), st, de);
+  const size_t lds_st = (2 * (size_t)Mmax + 64) * sizeof(double);
+  const unsigned nst = (unsigned)((Mmax + ST_T - 1) / ST_T), nto = (unsigned)((Mmax + 63) / 64);
+  hipLaunchKernelGGL(k_stebz, dim3(n, nst), dim3(ST_T), lds_st, st, de);
+  LC(hipGetLastError());
+  hipLaunchKernelGGL(k_stein, dim3(n, nst), dim3(ST_T), lds_st, st, de);
+  LC(hipGetLastError());
+  hipLaunchKernelGGL(k_stein_out, dim3(n, nto * nto), dim3(256), 0, st, de);
   LC(hipGetLastError());
   phase(2);
   // BCGS2 over panels of TNB eigenvectors (columns of Z = E.A)
@@ -891,6 +1136,8 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
         gemm(S, st, false, false, u);
       }
     }
+    hipLaunchKernelGGL(k_orth_panel, dim3(n), dim3(MG_T), 0, st, de, p);
+    LC(hipGetLastError());
     hipLaunchKernelGGL(k_mgs_panel, dim3(n), dim3(MG_T), 0, st, de, p);
     LC(hipGetLastError());
   }

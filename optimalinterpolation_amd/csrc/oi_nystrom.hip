@@ -111,9 +111,10 @@ __global__ void k_nys_eigpost(double* __restrict__ s, int64_t M, int64_t Mp, int
 }
 
 // ut = sqrt(M/n) * U1 / s  (column k divided by s[k]);  C = ut / sn2 (= Vi ut)
-__global__ void k_nys_ut(const double* __restrict__ U1, int64_t n, int64_t M,
+// (ut may alias U1: each element is read before it is written, by one thread)
+__global__ void k_nys_ut(const double* U1, int64_t n, int64_t M,
                          const double* __restrict__ s, double c, double isn2,
-                         double* __restrict__ ut, double* __restrict__ C) {
+                         double* ut, double* __restrict__ C) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n * M) return;
   const int64_t k = e / n;
@@ -624,7 +625,10 @@ class Runner {
     const int64_t mmaxp = mpmax_;
     ewd_ = oila::eigh_workspace_doubles((int)mmaxp);
     nd64_ = (mmaxp + 63) / 64;
-    const size_t per = (size_t)(6 * nmax + 2 * mmaxp * mmaxp + 2 * mmaxp + nmax * mmaxp) * 8 +
+    // OI_NYS_B3 (default 1): phase 3's two n x M products batched over the
+    // chunk (per-slot K_nm and U1 / ut) instead of one cell at a time per lane
+    if (const char* e = getenv("OI_NYS_B3")) b3_ = atoi(e) != 0;
+    const size_t per = (size_t)(6 * nmax + 2 * mmaxp * mmaxp + 2 * mmaxp + (b3_ ? 3 : 1) * nmax * mmaxp) * 8 +
                        (ewd_ + (size_t)nd64_ * 4096) * 8;
     size_t fr = 0, tot = 0;
     HC(hipMemGetInfo(&fr, &tot));
@@ -637,6 +641,10 @@ class Runner {
     eval_.alloc(ch * mmaxp * 8);
     stl_.alloc(ch * mmaxp * 8);
     C_.alloc(ch * nmax * mmaxp * 8);
+    if (b3_) {
+      Knm_.alloc(ch * nmax * mmaxp * 8);
+      U1_.alloc(ch * nmax * mmaxp * 8);
+    }
     B_.alloc(ch * mmaxp * mmaxp * 8);
     EW_.alloc(ch * ewd_ * 8);
     Dinv_.alloc(ch * nd64_ * 4096 * 8);
@@ -686,7 +694,10 @@ class Runner {
       const int64_t p1 = std::min(nc, p0 + chunk_);
       lanes_phase(p0, p1, 1);
       batched(p0, p1, 0);
-      lanes_phase(p0, p1, 3);
+      if (b3_)
+        batched3(p0, p1);
+      else
+        lanes_phase(p0, p1, 3);
       batched(p0, p1, 1);
       lanes_phase(p0, p1, 5);
     }
@@ -857,6 +868,57 @@ class Runner {
     return R;
   }
 
+  // phase 3 for a whole chunk on the main stream: the per-cell elementwise
+  // kernels, and each of the two n x M products as ONE batched oila::gemm over
+  // the chunk's cells (per-cell launches of ~1 000 64 x 64 tiles left the
+  // chip under-filled in the last wave of tiles)
+  void batched3(int64_t p0, int64_t p1) {
+    hipStream_t st = st_;
+    const int64_t nM = nmax_ * mpmax_;
+    double fl = 0.0, by = 0.0;
+    for (int64_t p = p0; p < p1; ++p) {
+      const CellRefs R = refs(p, p - p0);
+      fl += 4 * R.dn * R.dM * R.dM;
+      by += 8.0 * R.dn * R.dM;
+    }
+    sg_.begin(S_PANEL, fl, by);
+    std::vector<oila::Gemm> g1, g2;
+    for (int64_t p = p0; p < p1; ++p) {
+      const CellRefs R = refs(p, p - p0);
+      double* Knm = Knm_.as<double>() + (p - p0) * nM;
+      double* U1 = U1_.as<double>() + (p - p0) * nM;
+      hipLaunchKernelGGL(k_nys_eigpost, dim3(blocks(R.Mp, 256)), dim3(256), 0, st, R.s, R.M, R.Mp,
+                         R.n, R.stl);
+      KCHK();
+      hipLaunchKernelGGL(k_nys_cross, dim3(blocks(R.n, 256), (unsigned)R.M), dim3(256), 0, st, R.sc,
+                         nullptr, R.n, R.sc, R.sl, R.hp[3], Knm, R.n);
+      KCHK();
+      g1.push_back(oila::Gemm{Knm, R.Kmm, U1, R.in, R.iM, R.iM, R.in, R.iMp, R.in, 1.0, 0.0, 0});  // U1 = Knm u
+      g2.push_back(oila::Gemm{U1, R.C, R.B, R.iM, R.iM, R.in, R.in, R.in, R.iMp, 1.0, 0.0, 0});    // B = ut' C
+    }
+    oila::gemm(la_, st, false, false, g1);
+    for (int64_t p = p0; p < p1; ++p) {  // ut (in place of U1) and C
+      const CellRefs R = refs(p, p - p0);
+      double* U1 = U1_.as<double>() + (p - p0) * nM;
+      hipLaunchKernelGGL(k_nys_ut, dim3(blocks(R.n * R.M, 256)), dim3(256), 0, st, U1, R.n, R.M, R.s,
+                         std::sqrt(R.dM / R.dn), 1.0 / R.hp[4], U1, R.C);
+      KCHK();
+    }
+    oila::gemm(la_, st, true, false, g2);
+    for (int64_t p = p0; p < p1; ++p) {  // B += diag(1/st), pad block
+      const CellRefs R = refs(p, p - p0);
+      hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.M, 256)), dim3(256), 0, st, R.B, R.M, R.Mp, R.stl, 1,
+                         0.0);
+      KCHK();
+      if (R.Mp > R.M) {
+        hipLaunchKernelGGL(k_nys_pad, dim3(blocks(R.Mp, 256), (unsigned)R.Mp), dim3(256), 0, st, R.B,
+                           R.M, R.Mp, 1.0);
+        KCHK();
+      }
+    }
+    sg_.end();
+  }
+
   // scaled inputs, Kmm (NB1 Nystroem: SGPkernel(x[sel]))
   void phase1(Lane& L, int64_t p, int64_t slot) {
     const CellRefs R = refs(p, slot);
@@ -999,7 +1061,8 @@ class Runner {
   hipStream_t st_;
   bool obj_ = false, pred_ = false, alloc_obj_, alloc_pred_;
   Buf res_, info_;
-  Buf sc_, sq_, Kmm_, eval_, stl_, C_, B_, EW_, Dinv_;
+  Buf sc_, sq_, Kmm_, eval_, stl_, C_, B_, EW_, Dinv_, Knm_, U1_;
+  bool b3_ = true;
   int64_t chunk_ = 1;
   int padq_ = 32;
   int64_t mpmax_ = 0;

@@ -12,8 +12,9 @@ kernels run.
   3. eigenvectors of the tridiagonal by inverse iteration with partial
      pivoting (dlagtf / dlagts), a pseudo-random start per eigenvalue;
   4. block classical Gram-Schmidt twice (BCGS2) over panels of 32 vectors,
-     modified Gram-Schmidt inside a panel, a fresh start vector where one
-     collapses (numerically repeated eigenvalues);
+     Cholesky QR twice inside a panel; where a column collapses (numerically
+     repeated eigenvalues) Gram-Schmidt column by column with a fresh start
+     vector;
   5. back-transform U = Q Z, one block reflector I - V T V' per panel.
 """
 import numpy as np
@@ -187,6 +188,41 @@ def stein(d, e, lam, tnorm, iters=2):
     return Z
 
 
+def mgs(Z, p, q):
+    M = Z.shape[0]
+    for j in range(p, q):
+        for tries in range(3):
+            n0 = np.linalg.norm(Z[:, j])
+            for _ in range(2):
+                Z[:, j] -= Z[:, p:j] @ (Z[:, p:j].T @ Z[:, j])
+            n1 = np.linalg.norm(Z[:, j])
+            if n1 > 1e-2 * n0:
+                break
+            x = start_vector(j + 7919 * (tries + 1), M)
+            for _ in range(2):
+                x -= Z[:, :j] @ (Z[:, :j].T @ x)
+            Z[:, j] = x
+        Z[:, j] /= np.linalg.norm(Z[:, j])
+
+
+def cholqr2(Z, p, q):
+    """Z[:, p:q] <- Q of its QR, twice (k_orth_panel); False on a collapse
+    (a pivot keeping <= 1e-4 of its column's squared norm), Z then unchanged
+    by the failing pass."""
+    for _ in range(2):
+        G = Z[:, p:q].T @ Z[:, p:q]
+        R = np.triu(G).copy()
+        nb = q - p
+        for j in range(nb):
+            if not R[j, j] > 1e-4 * G[j, j]:
+                return False
+            R[j, j] = np.sqrt(R[j, j])
+            R[j, j + 1:] /= R[j, j]
+            R[j + 1:, j + 1:] -= np.triu(np.outer(R[j, j + 1:], R[j, j + 1:]))
+        Z[:, p:q] = Z[:, p:q] @ np.linalg.inv(R)
+    return True
+
+
 def bcgs2(Z, nb=32):
     M, K = Z.shape
     Z = Z.copy()
@@ -195,19 +231,8 @@ def bcgs2(Z, nb=32):
         for _ in range(2):
             H = Z[:, :p].T @ Z[:, p:q]
             Z[:, p:q] -= Z[:, :p] @ H
-        for j in range(p, q):
-            for tries in range(3):
-                n0 = np.linalg.norm(Z[:, j])
-                for _ in range(2):
-                    Z[:, j] -= Z[:, p:j] @ (Z[:, p:j].T @ Z[:, j])
-                n1 = np.linalg.norm(Z[:, j])
-                if n1 > 1e-2 * n0:
-                    break
-                x = start_vector(j + 7919 * (tries + 1), M)
-                for _ in range(2):
-                    x -= Z[:, :j] @ (Z[:, :j].T @ x)
-                Z[:, j] = x
-            Z[:, j] /= np.linalg.norm(Z[:, j])
+        if not cholqr2(Z, p, q):
+            mgs(Z, p, q)
     return Z
 
 

@@ -1,0 +1,87 @@
+// Phase times of oila::eigh on a chunk of Matern K_mm matrices (the Nystrom
+// variant's M = 925 padded to 928, 32 per chunk), plus the per-phase cycle
+// split of k_sytrd on matrix 0 (build: see tools/build_eigh_probe.sh).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../optimalinterpolation_amd/csrc/oi_linalg.h"
+
+extern "C" int oila_sytrd_cycles(unsigned long long* out);
+
+#define CK(x)                                                             \
+  do {                                                                    \
+    hipError_t e_ = (x);                                                  \
+    if (e_ != hipSuccess) {                                               \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));             \
+      return 1;                                                           \
+    }                                                                     \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 928, nb = argc > 2 ? atoi(argv[2]) : 32, reps = 3;
+  std::mt19937_64 rng(7);
+  std::uniform_real_distribution<double> U(-3e5, 3e5), Tt(0, 8);
+  const size_t MM = (size_t)M * M, ew = oila::eigh_workspace_doubles(M);
+  std::vector<double> h(MM * nb);
+  for (int b = 0; b < nb; ++b) {
+    std::vector<double> x(3 * M);
+    for (int i = 0; i < M; ++i) {
+      x[3 * i] = U(rng) / 5e4;
+      x[3 * i + 1] = U(rng) / 5e4;
+      x[3 * i + 2] = Tt(rng) / 1.0;
+    }
+    for (int j = 0; j < M; ++j)
+      for (int i = 0; i < M; ++i) {
+        double d = 0;
+        for (int q = 0; q < 3; ++q) d += (x[3 * i + q] - x[3 * j + q]) * (x[3 * i + q] - x[3 * j + q]);
+        const double Q = std::sqrt(3.0 * d);
+        h[MM * b + i + (size_t)M * j] = 6e-3 * (1 + Q) * std::exp(-Q) + (i == j ? 1e-4 : 0.0);
+      }
+  }
+  double *A, *A0, *w, *work;
+  CK(hipMalloc(&A, MM * nb * 8));
+  CK(hipMalloc(&A0, MM * nb * 8));
+  CK(hipMalloc(&w, (size_t)M * nb * 8));
+  CK(hipMalloc(&work, ew * nb * 8));
+  CK(hipMemcpy(A0, h.data(), MM * nb * 8, hipMemcpyHostToDevice));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  oila::Stager S;
+  S.bind(st);
+  std::vector<oila::Eigh> es;
+  for (int b = 0; b < nb; ++b) es.push_back(oila::Eigh{A + MM * b, w + (size_t)M * b, work + ew * b, M, M});
+  hipEvent_t ev[5];
+  for (auto& e : ev) CK(hipEventCreate(&e));
+  double ph[4] = {0, 0, 0, 0};
+  for (int r = 0; r <= reps; ++r) {
+    CK(hipMemcpyAsync(A, A0, MM * nb * 8, hipMemcpyDeviceToDevice, st));
+    oila::eigh(S, st, es, [&](int k) { (void)hipEventRecord(ev[k], st); });
+    CK(hipStreamSynchronize(st));
+    S.reset();
+    if (r == 0) continue;  // warm-up
+    for (int k = 0; k < 4; ++k) {
+      float ms;
+      CK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      ph[k] += ms / reps;
+    }
+  }
+  printf("eigh M=%d x %d: sytrd %.2f ms, stebz+stein %.2f ms, orth %.2f ms, back %.2f ms\n", M, nb, ph[0],
+         ph[1], ph[2], ph[3]);
+  unsigned long long cyc[8];
+  if (oila_sytrd_cycles(cyc) == 0) {
+    const char* nm[7] = {"col update", "dlarfg", "symv", "panel gemv", "w + T col", "T store", "trailing"};
+    double tot = 0;
+    for (int k = 0; k < 7; ++k) tot += cyc[k];
+    for (int k = 0; k < 7; ++k) printf("  sytrd %-10s %5.1f %%  (%.2f Mcycles per call)\n", nm[k], 100.0 * cyc[k] / tot,
+                                       cyc[k] / 1e6 / (reps + 1));
+  }
+  std::vector<double> wh((size_t)M * nb);
+  CK(hipMemcpy(wh.data(), w, wh.size() * 8, hipMemcpyDeviceToHost));
+  printf("eigenvalues of matrix 0: min %.3e max %.3e\n", wh[0], wh[M - 1]);
+  return 0;
+}
