@@ -59,6 +59,30 @@ namespace oila {
     if (e_ != hipSuccess) throw LinalgErr{std::string(#expr) + ": " + hipGetErrorString(e_)}; \
   } while (0)
 
+// Global-address-space views of the descriptors' pointers: plain accesses
+// through generic pointers compile to flat_* instructions, which count
+// against lgkmcnt too, so every LDS wait would also wait for the loads in
+// flight (the prefetch of the next chunk, the symv's batch) -- G() makes them
+// global_* instructions, counted by vmcnt only.
+typedef __attribute__((address_space(1))) double gdouble;
+__device__ __forceinline__ gdouble* G(double* p) { return (gdouble*)p; }
+__device__ __forceinline__ const gdouble* G(const double* p) { return (const gdouble*)p; }
+
+// Masked loads without branches: a raw buffer load whose offset is pushed
+// past the descriptor's range returns 0 (hardware bounds check) -- a plain
+// load under a condition becomes an exec-masked branch per load with a
+// vmcnt(0) wait in it, which serialises the batch.  Descriptors are built
+// from wave-uniform base pointers; offsets are in bytes from that base and
+// must stay below 2 GiB (one matrix / panel per descriptor).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc rsrc(const double* p) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ double bload(Rsrc r, bool ok, size_t idx) {
+  const unsigned off = ok ? (unsigned)(idx * 8) : 0xFFFFFFF0u;
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
 // ------------------------------------------------------------------ k_gemm
 #define GT 64
 #define GKC 16
@@ -81,6 +105,7 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
   quad_zero(acc);
   const int nch = (kmax + GKC - 1) / GKC;
   double ra[4], rb[4];
+  const Rsrc rA = rsrc(g.A), rB = rsrc(g.B);
   // element e = t + 256 q of a 64 x 16 chunk: A(m, k) and op(B)(k, n)
   auto load = [&](int ch) __attribute__((always_inline)) {
     const int k0 = ch * GKC;
@@ -90,11 +115,11 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
       int m, k;
       if (TA) { k = e & 15; m = e >> 4; } else { m = e & 63; k = e >> 6; }
       const int gm = m0 + m, gk = k0 + k;
-      ra[q] = (gm < g.m && gk < kmax) ? (TA ? g.A[gk + (size_t)g.lda * gm] : g.A[gm + (size_t)g.lda * gk]) : 0.0;
+      ra[q] = bload(rA, gm < g.m && gk < kmax, TA ? gk + (size_t)g.lda * gm : gm + (size_t)g.lda * gk);
       int n, kb;
       if (TB) { n = e & 63; kb = e >> 6; } else { kb = e & 15; n = e >> 4; }
       const int gn = n0 + n, gkb = k0 + kb;
-      rb[q] = (gn < g.n && gkb < kmax) ? (TB ? g.B[gn + (size_t)g.ldb * gkb] : g.B[gkb + (size_t)g.ldb * gn]) : 0.0;
+      rb[q] = bload(rB, gn < g.n && gkb < kmax, TB ? gn + (size_t)g.ldb * gkb : gkb + (size_t)g.ldb * gn);
     }
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
@@ -144,7 +169,7 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
   for (int e = t; e < GT * GT; e += 256) {
     const int m = e & 63, n = e >> 6, gm = m0 + m, gn = n0 + n;
     if (gm >= g.m || gn >= g.n) continue;
-    double* c = g.C + gm + (size_t)g.ldc * gn;
+    gdouble* c = G(g.C) + gm + (size_t)g.ldc * gn;
     const double v = g.alpha * X[n * 65 + m];
     *c = g.beta == 0.0 ? v : v + g.beta * *c;
   }
@@ -184,7 +209,7 @@ __global__ __launch_bounds__(64) void k_potrf_tile(const Chol* __restrict__ cs, 
   const Chol c = cs[blockIdx.x];
   if (jb >= c.M) return;
   const int nb = min(64, c.M - jb), r = threadIdx.x;
-  double* A = c.A + jb + (size_t)c.lda * jb;
+  gdouble* A = G(c.A) + jb + (size_t)c.lda * jb;
   for (int j = 0; j < 64; ++j)
     L[r * 65 + j] = (r < nb && j < nb) ? (j <= r ? A[r + (size_t)c.lda * j] : 0.0) : (r == j ? 1.0 : 0.0);
   __syncthreads();
@@ -205,7 +230,7 @@ __global__ __launch_bounds__(64) void k_potrf_tile(const Chol* __restrict__ cs, 
   }
   if (bad && r == 0) *c.info = 1;
   // inverse: lane j forms column j of L^-1 by forward substitution
-  double* D = c.dinv + (size_t)(jb / 64) * 4096;
+  gdouble* D = G(c.dinv) + (size_t)(jb / 64) * 4096;
   {
     const int j = r;
     double x[64];
@@ -252,6 +277,13 @@ __host__ __device__ inline EighWs carve(double* w, int M) {
   s.tau = s.e + M + 1;
   s.flag = s.tau + M + 1;  // k_orth_panel -> k_mgs_panel: the panel collapsed
   return s;
+}
+struct EighWsG {  // carve() as global-address-space pointers (device side)
+  gdouble *Vc, *Ws, *T, *d, *e, *tau, *scr, *H, *X, *Y, *flag;
+};
+__device__ inline EighWsG carveG(double* w, int M) {
+  const EighWs s = carve(w, M);
+  return EighWsG{G(s.Vc), G(s.Ws), G(s.T), G(s.d), G(s.e), G(s.tau), G(s.scr), G(s.H), G(s.X), G(s.Y), G(s.flag)};
 }
 size_t eigh_workspace_doubles(int M) {
   const size_t MM = (size_t)M * M;
@@ -304,13 +336,15 @@ __device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] =
 __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ es, int p) {
   extern __shared__ double sm[];
   const Eigh E = es[blockIdx.x];
-  const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // provably wave-uniform (buffer descriptors)
   if (p >= M - 1) {
     if (p == 0 && t == 0) ws_d0(E);  // M == 1
     return;
   }
-  double* A = E.A;
-  EighWs ws = carve(E.work, M);
+  gdouble* A = G(E.A);
+  EighWsG ws = carveG(E.work, M);
+  const Rsrc rV = rsrc(carve(E.work, M).Vc + (size_t)M * p), rW = rsrc(carve(E.work, M).Ws);  // panel V, W
   double* yw = sm;
   double* v = yw + (size_t)SY_W * M;
   double* y = v + M;
@@ -329,15 +363,21 @@ __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ e
       const int g = p + i;
       // (1) column g with the panel's previous columns: A(r,g) -= V(r,q) W(g,q) + W(r,q) V(g,q)
       if (i > 0) {
-        for (int r = g + t; r < M; r += SY_T) {
-          double s = A[r + (size_t)ld * g];
-#pragma unroll 16
+        // two rows per thread (ra, ra + SY_T), buffer loads: 32 in flight per lane
+        for (int ra = g + t; ra < M; ra += 2 * SY_T) {
+          const int rb = ra + SY_T;
+          const bool okb = rb < M;
+          double sa = A[ra + (size_t)ld * g], sb = okb ? A[rb + (size_t)ld * g] : 0.0;
+#pragma unroll 8
           for (int q = 0; q < i; ++q) {
-            const double* vq = ws.Vc + (size_t)M * (p + q);
-            const double* wq = ws.Ws + (size_t)M * q;
-            s -= vq[r] * wq[g] + wq[r] * vq[g];
+            const double wg = ws.Ws[(size_t)M * q + g], vg = ws.Vc[(size_t)M * (p + q) + g];
+            const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
+            const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
+            sa -= va * wg + wa * vg;
+            sb -= vb * wg + wb * vg;
           }
-          A[r + (size_t)ld * g] = s;
+          A[ra + (size_t)ld * g] = sa;
+          if (okb) A[rb + (size_t)ld * g] = sb;
         }
         __syncthreads();
       }
@@ -361,7 +401,7 @@ __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ e
         tau = (beta - alpha) / beta;
         scal = 1.0 / (alpha - beta);
       }
-      double* vg = ws.Vc + (size_t)M * g;
+      gdouble* vg = ws.Vc + (size_t)M * g;
       for (int r = t; r < M; r += SY_T) {
         const double x = r < g + 1 ? 0.0 : r == g + 1 ? 1.0 : A[r + (size_t)ld * g] * scal;
         v[r] = x;
@@ -383,7 +423,7 @@ __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ e
       // group's column dots are reduced once at its end
       double* myw = yw + (size_t)wv * M;
       for (int c0 = g + 1 + SY_C * wv; c0 < M; c0 += SY_C * SY_W) {
-        const double* col = A + (size_t)ld * c0;
+        const Rsrc rcol = rsrc(E.A + (size_t)ld * c0);
         double vc[SY_C], dot[SY_C];
 #pragma unroll
         for (int j = 0; j < SY_C; ++j) {
@@ -396,8 +436,10 @@ __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ e
           for (int u = 0; u < SY_R; ++u)
 #pragma unroll
             for (int j = 0; j < SY_C; ++j) {
+              // unconditional loads from clamped addresses (a branch per load
+              // would serialise them), masked afterwards
               const int r = r0 + lane + 64 * u;
-              a[u][j] = (r < M && r >= c0 + j) ? col[r + (size_t)ld * j] : 0.0;
+              a[u][j] = bload(rcol, r < M && r >= c0 + j, r + (size_t)ld * j);
             }
 #pragma unroll
           for (int u = 0; u < SY_R; ++u) {
@@ -426,7 +468,7 @@ __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ e
       // panel corrections: pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g)
       // (4 dots per wave at a time, 4 row chunks each: 16 loads per lane in flight)
       for (int jq0 = 4 * wv; jq0 < 2 * i; jq0 += 4 * SY_W) {
-        const double* col[4];
+        const gdouble* col[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           const int jq = min(jq0 + d, 2 * i - 1), q = jq % i;
@@ -442,10 +484,13 @@ __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ e
 #pragma unroll
           for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int d = 0; d < 4; ++d) a[d][u] = r + 64 * u < M ? col[d][r + 64 * u] : 0.0;
+            for (int d = 0; d < 4; ++d) {
+              const double x = col[d][min(r + 64 * u, M - 1)];
+              a[d][u] = r + 64 * u < M ? x : 0.0;
+            }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const double vr = r + 64 * u < M ? v[r + 64 * u] : 0.0;
+            const double vr = r + 64 * u < M ? v[min(r + 64 * u, M - 1)] : 0.0;
 #pragma unroll
             for (int d = 0; d < 4; ++d) s4[d][u] += a[d][u] * vr;
           }
@@ -473,30 +518,45 @@ __global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ e
       }
       // (4) w = tau (y - V (W'v) - W (V'v)), then w += -tau/2 (w'v) v
       double sv[1] = {0.0};
-      for (int r = g + 1 + t; r < M; r += SY_T) {
-        double s = 0.0;
+      for (int ra = g + 1 + t; ra < M; ra += 2 * SY_T) {
+        const int rb = ra + SY_T;
+        const bool okb = rb < M;
+        double sa = 0.0, sb = 0.0;
 #pragma unroll
         for (int ww = 0; ww < SY_W; ++ww) {
-          s += yw[(size_t)ww * M + r];
-          yw[(size_t)ww * M + r] = 0.0;
+          sa += yw[(size_t)ww * M + ra];
+          yw[(size_t)ww * M + ra] = 0.0;
+          if (okb) {
+            sb += yw[(size_t)ww * M + rb];
+            yw[(size_t)ww * M + rb] = 0.0;
+          }
         }
-#pragma unroll 16
-        for (int q = 0; q < i; ++q)
-          s -= ws.Vc[(size_t)M * (p + q) + r] * pan[q] + ws.Ws[(size_t)M * q + r] * pan[TNB + q];
-        const double wr = tau * s;
-        y[r] = wr;
-        sv[0] += wr * v[r];
+#pragma unroll 8
+        for (int q = 0; q < i; ++q) {
+          const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
+          const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
+          sa -= va * pan[q] + wa * pan[TNB + q];
+          sb -= vb * pan[q] + wb * pan[TNB + q];
+        }
+        const double wra = tau * sa;
+        y[ra] = wra;
+        sv[0] += wra * v[ra];
+        if (okb) {
+          const double wrb = tau * sb;
+          y[rb] = wrb;
+          sv[0] += wrb * v[rb];
+        }
       }
       wg_sum<1>(sv, red);
       const double a2 = -0.5 * tau * sv[0];
-      double* wcol = ws.Ws + (size_t)M * i;
+      gdouble* wcol = ws.Ws + (size_t)M * i;
       for (int r = t; r < M; r += SY_T) wcol[r] = r <= g ? 0.0 : y[r] + a2 * v[r];
       __syncthreads();
     }
     SY_STAMP(4);
     // T of the block reflector H_p ... H_{p+nb-1} = I - V T V' (formed column
     // by column in step (4)) to the workspace for the back-transform
-    double* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
+    gdouble* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
     for (int e = t; e < TNB * TNB; e += SY_T) {
       Tp[e] = Tl[e];
       Tl[e] = 0.0;
@@ -526,7 +586,7 @@ __device__ __forceinline__ double start_value(int k, int i) {
 // serial chains per thread, so the batch is spread over the whole chip.
 // dynamic LDS: d[M] | e2[M] | red[64]
 #define ST_T 64
-__device__ __forceinline__ void tri_setup(const Eigh& E, const EighWs& ws, double* d, double* e2, double* red) {
+__device__ __forceinline__ void tri_setup(const Eigh& E, const EighWsG& ws, double* d, double* e2, double* red) {
   const int M = E.M, t = threadIdx.x;
   for (int i = t; i < M; i += ST_T) {
     d[i] = ws.d[i];
@@ -556,7 +616,7 @@ __global__ __launch_bounds__(ST_T) void k_stebz(const Eigh* __restrict__ es) {
   const Eigh E = es[blockIdx.x];
   const int M = E.M, t = threadIdx.x;
   if ((int)blockIdx.y * ST_T >= M) return;
-  EighWs ws = carve(E.work, M);
+  EighWsG ws = carveG(E.work, M);
   double* d = sm;
   double* e2 = d + M;
   double* red = e2 + M;
@@ -583,7 +643,7 @@ __global__ __launch_bounds__(ST_T) void k_stebz(const Eigh* __restrict__ es) {
       if (cnt <= k) lo = mid;
       else hi = mid;
     }
-    E.w[k] = 0.5 * (lo + hi);
+    G(E.w)[k] = 0.5 * (lo + hi);
   }
 }
 
@@ -594,7 +654,8 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
   const Eigh E = es[blockIdx.x];
   const int M = E.M, t = threadIdx.x;
   if ((int)blockIdx.y * ST_T >= M) return;
-  EighWs ws = carve(E.work, M);
+  EighWsG ws = carveG(E.work, M);
+  const gdouble* w = G(E.w);
   double* d = sm;
   double* e2 = d + M;
   double* red = e2 + M;
@@ -602,12 +663,12 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
   const double tnorm = red[2];
   const double eps = 2.220446049250313e-16;
   const size_t MM = (size_t)M * M;
-  double* sa = ws.scr;          // U diagonal
-  double* sb = sa + MM;         // U first superdiagonal
-  double* sc = sb + MM;         // U second superdiagonal
-  double* sl = sc + MM;         // L multipliers
-  double* sp = sl + MM;         // row interchange flags
-  double* sx = sp + MM;         // iterate
+  gdouble* sa = ws.scr;          // U diagonal
+  gdouble* sb = sa + MM;         // U first superdiagonal
+  gdouble* sc = sb + MM;         // U second superdiagonal
+  gdouble* sl = sc + MM;         // L multipliers
+  gdouble* sp = sl + MM;         // row interchange flags
+  gdouble* sx = sp + MM;         // iterate
   // The bottom cluster: eigenvalues 0 .. nb0-1 whose consecutive gaps are all
   // <= 1e3 eps ||T|| -- the numerical null space of a rank-deficient K_mm
   // (duplicated sites) and the noise band below it.  Inverse iteration cannot
@@ -620,7 +681,7 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
   if (t == 0) {
     const double gtol = 1e3 * eps * tnorm;
     int nb0 = 1;
-    while (nb0 < M && E.w[nb0] - E.w[nb0 - 1] <= gtol) ++nb0;
+    while (nb0 < M && w[nb0] - w[nb0 - 1] <= gtol) ++nb0;
     red[4] = nb0 >= 2 ? (double)nb0 : 0.0;
   }
   __syncthreads();
@@ -628,7 +689,7 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
   {
     const int k = (int)blockIdx.y * ST_T + t;
     if (k >= M) return;
-    const double lam = E.w[k];
+    const double lam = w[k];
     if (k < nb0) {
       double nrm = 0.0;
       for (int i = 0; i < M; ++i) {
@@ -730,8 +791,8 @@ __global__ __launch_bounds__(256) void k_stein_out(const Eigh* __restrict__ es) 
   const Eigh E = es[blockIdx.x];
   const int M = E.M, nt = (M + 63) / 64;
   if ((int)blockIdx.y >= nt * nt) return;
-  const EighWs ws = carve(E.work, M);
-  const double* sx = ws.scr + 5 * (size_t)M * M;
+  const EighWsG ws = carveG(E.work, M);
+  const gdouble* sx = ws.scr + 5 * (size_t)M * M;
   const int i0 = 64 * ((int)blockIdx.y % nt), k0 = 64 * ((int)blockIdx.y / nt), t = threadIdx.x;
   for (int e = t; e < 64 * 64; e += 256) {
     const int i = i0 + e / 64, k = k0 + e % 64;
@@ -740,7 +801,7 @@ __global__ __launch_bounds__(256) void k_stein_out(const Eigh* __restrict__ es) 
   __syncthreads();
   for (int e = t; e < 64 * 64; e += 256) {
     const int i = i0 + e % 64, k = k0 + e / 64;
-    if (i < M && k < M) E.A[i + (size_t)E.lda * (M - 1 - k)] = tile[e % 64][e / 64];
+    if (i < M && k < M) G(E.A)[i + (size_t)E.lda * (M - 1 - k)] = tile[e % 64][e / 64];
   }
 }
 
@@ -771,7 +832,7 @@ __global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es,
   const int M = E.M;
   if (p >= M || carve(E.work, M).flag[0] == 0.0) return;  // k_orth_panel's Cholesky QR held
   const int q = min(M, p + TNB), t = threadIdx.x, lane = t & 63, w = t >> 6;
-  double* Z = E.A;
+  gdouble* Z = G(E.A);
   const size_t ld = E.lda;
   auto reduce = [&](double (&v)[33]) {  // fixed-order sums of 33 values
 #pragma unroll
@@ -787,7 +848,7 @@ __global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es,
     __syncthreads();
   };
   for (int j = p; j < q; ++j) {
-    double* zj = Z + ld * j;
+    gdouble* zj = Z + ld * j;
     for (int attempt = 0; attempt < 4; ++attempt) {
       const int lo = attempt == 0 ? p : 0;  // a fresh vector is projected out of everything
       double dv[33];
@@ -852,10 +913,11 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
   const Eigh E = es[blockIdx.x];
   const int M = E.M;
   if (p >= M) return;
-  const int nb = min(TNB, M - p), t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nb = min(TNB, M - p), t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int fr = lane & 15, fk = lane >> 4;
   const size_t ld = E.lda;
-  double* Z = E.A + ld * p;
+  gdouble* Z = G(E.A) + ld * p;
+  const Rsrc rz = rsrc(E.A + ld * p);
   if (t == 0) carve(E.work, M).flag[0] = 0.0;
   for (int pass = 0; pass < 2; ++pass) {
     // (1) G = Z_p' Z_p: wave w sums the 16-row blocks 16 (w + 4 j), 4 k-steps per batch
@@ -866,8 +928,8 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = i0 + 4 * u + fk;
-        a0[u] = (i < M && fr < nb) ? Z[i + ld * fr] : 0.0;
-        a1[u] = (i < M && 16 + fr < nb) ? Z[i + ld * (16 + fr)] : 0.0;
+        a0[u] = bload(rz, i < M && fr < nb, i + ld * fr);
+        a1[u] = bload(rz, i < M && 16 + fr < nb, i + ld * (16 + fr));
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -944,7 +1006,7 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
 #pragma unroll
       for (int kk = 0; kk < TNB / 4; ++kk) {
         const int i = i0 + fr, a = 4 * kk + fk;
-        za[kk] = (i < M && a < nb) ? Z[i + ld * a] : 0.0;
+        za[kk] = bload(rz, i < M && a < nb, i + ld * a);
       }
       d4 o0 = (d4){0.0, 0.0, 0.0, 0.0}, o1 = o0;
 #pragma unroll
