@@ -13,14 +13,14 @@
 //   k_potrf_tile  Cholesky + inverse of one 64 x 64 diagonal block per matrix
 //                 (the blocked right-looking factorisation: potrf_tile ->
 //                 panel product with the block inverse -> lower-tile update)
-//   k_sytrd       Householder tridiagonalisation (LAPACK dsytrd / dlatrd,
-//                 lower) of one matrix per 512-thread workgroup: per column
-//                 the symmetric product over the trailing lower triangle (each
-//                 wave owns columns; the transposed half is accumulated in
-//                 per-wave LDS vectors, summed in fixed order), panel
-//                 corrections, then the rank-2*32 trailing update per panel on
-//                 the MFMA core; V (unit lower, clean copy) and T (dlarft,
-//                 forward columnwise) kept per 32-column panel
+//   k_sy_reflect / k_sy_symv / k_sy_w
+//                 Householder tridiagonalisation (LAPACK dsytrd / dlatrd,
+//                 lower), three launches per column over the batch: the
+//                 column's reflector, the symmetric product over the trailing
+//                 lower triangle on SY_S workgroups per matrix, the w vector;
+//                 per 32-column panel the rank-64 trailing update on k_gemm;
+//                 V (unit lower, clean copy) and T (dlarft, forward
+//                 columnwise) kept per panel
 //   k_stebz       eigenvalues of the tridiagonal by bisection on Sturm counts
 //                 (dstebz), one thread per eigenvalue
 //   k_stein       eigenvectors by inverse iteration with partial pivoting
@@ -311,257 +311,241 @@ __device__ __forceinline__ void wg_sum(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
-// phase cycle counts of matrix 0 (tools/eigh_probe.cpp builds with OI_SYTRD_TIMING)
-#ifdef OI_SYTRD_TIMING
-__device__ unsigned long long g_sy_cycles[8];
-#define SY_STAMP(k)                                                        \
-  do {                                                                     \
-    __syncthreads();                                                       \
-    if (blockIdx.x == 0 && threadIdx.x == 0) {                             \
-      const unsigned long long now_ = clock64();                           \
-      g_sy_cycles[k] += now_ - sy_last_;                                   \
-      sy_last_ = now_;                                                     \
-    }                                                                      \
-  } while (0)
-extern "C" int oila_sytrd_cycles(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sy_cycles), sizeof(g_sy_cycles)) == hipSuccess ? 0 : -1;
-}
-#else
-#define SY_STAMP(k) do {} while (0)
-#endif
-// dynamic LDS: yw[SY_W][M] | v[M] | y[M] | red[64] | pan[2 * TNB] | Tl[TNB * TNB]
+// dynamic LDS: yw[SY_W][M] | v[M] | red[64]
 __device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] = E.A[0]; }
-// Panel p (columns p .. p+nb-1) of the tridiagonalisation, one workgroup per
-// matrix; the panel's trailing update runs after it on oila::gemm.
-__global__ __launch_bounds__(SY_T) void k_sytrd_panel(const Eigh* __restrict__ es, int p) {
-  extern __shared__ double sm[];
+
+// The tridiagonalisation runs column by column as three launches per column
+// g = p + i (panel p, i < 32) over the whole batch -- the symmetric product
+// y = A22 v streams the trailing lower triangle once per column, and one
+// workgroup per matrix could pull it only at ~40 GB/s (a CU's outstanding
+// misses bound it; measured round 4), so it is spread over SY_S workgroups
+// per matrix:
+//   k_sy_reflect(p, i)  column g brought up to date with the panel's earlier
+//                       reflectors, the reflector v_g (dlarfg): d, e, tau, V
+//   k_sy_symv(p, i)     partial y of SY_S workgroups (their waves own groups of
+//                       SY_C consecutive columns) and the panel dots V'v, W'v
+//   k_sy_w(p, i)        y summed in a fixed order, w = tau (y - V(W'v) - W(V'v))
+//                       - tau/2 (w'v) v, column i of the panel's T (dlarft)
+// then, per panel, the trailing update A22 -= V W' + W V' on oila::gemm.
+#define SY_S 8  // symv workgroups per matrix
+__global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es, int p, int i) {
+  __shared__ double red[64];
   const Eigh E = es[blockIdx.x];
-  const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // provably wave-uniform (buffer descriptors)
+  const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i;
   if (p >= M - 1) {
-    if (p == 0 && t == 0) ws_d0(E);  // M == 1
+    if (p == 0 && i == 0 && t == 0) ws_d0(E);  // M == 1
     return;
   }
+  if (g >= M - 1) return;  // this matrix's last panel is shorter
   gdouble* A = G(E.A);
   EighWsG ws = carveG(E.work, M);
   const Rsrc rV = rsrc(carve(E.work, M).Vc + (size_t)M * p), rW = rsrc(carve(E.work, M).Ws);  // panel V, W
+  // (1) A(r,g) -= V(r,q) W(g,q) + W(r,q) V(g,q), q < i; two rows per thread
+  if (i > 0) {
+    for (int ra = g + t; ra < M; ra += 2 * SY_T) {
+      const int rb = ra + SY_T;
+      const bool okb = rb < M;
+      double sa = A[ra + (size_t)ld * g], sb = okb ? A[rb + (size_t)ld * g] : 0.0;
+#pragma unroll 8
+      for (int q = 0; q < i; ++q) {
+        const double wg = ws.Ws[(size_t)M * q + g], vg = ws.Vc[(size_t)M * (p + q) + g];
+        const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
+        const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
+        sa -= va * wg + wa * vg;
+        sb -= vb * wg + wb * vg;
+      }
+      A[ra + (size_t)ld * g] = sa;
+      if (okb) A[rb + (size_t)ld * g] = sb;
+    }
+    __syncthreads();
+  }
+  // (2) reflector annihilating A(g+2:M, g) (dlarfg)
+  double xs[1] = {0.0};
+  for (int r = g + 2 + t; r < M; r += SY_T) {
+    const double a = A[r + (size_t)ld * g];
+    xs[0] += a * a;
+  }
+  wg_sum<1>(xs, red);
+  const double alpha = A[g + 1 + (size_t)ld * g];
+  const double xn = sqrt(xs[0]);
+  double tau, beta, scal;
+  if (xn == 0.0) {
+    tau = 0.0;
+    beta = alpha;
+    scal = 0.0;
+  } else {
+    beta = -copysign(sqrt(alpha * alpha + xn * xn), alpha);
+    tau = (beta - alpha) / beta;
+    scal = 1.0 / (alpha - beta);
+  }
+  gdouble* vg = ws.Vc + (size_t)M * g;
+  for (int r = t; r < M; r += SY_T) vg[r] = r < g + 1 ? 0.0 : r == g + 1 ? 1.0 : A[r + (size_t)ld * g] * scal;
+  if (t == 0) {
+    ws.d[g] = A[g + (size_t)ld * g];
+    ws.e[g] = beta;
+    ws.tau[g] = tau;
+  }
+}
+
+// partial y of workgroup s into H[s M + r] (rows g+1 .. M-1); the panel dots
+// pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g) into X[0 .. 2 TNB)
+__global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, int p, int i) {
+  extern __shared__ double sm[];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63, g = p + i, sgrp = blockIdx.y;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // provably wave-uniform (buffer descriptors)
+  if (g >= M - 1) return;
+  EighWsG ws = carveG(E.work, M);
   double* yw = sm;
   double* v = yw + (size_t)SY_W * M;
-  double* y = v + M;
-  double* red = y + M;
-  double* pan = red + 64;  // pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v
-  double* Tl = pan + 2 * TNB; // TNB x TNB: T of the current panel's block reflector
-  for (int i = t; i < SY_W * M; i += SY_T) yw[i] = 0.0;
-  for (int i = t; i < TNB * TNB; i += SY_T) Tl[i] = 0.0;
+  for (int r = t; r < SY_W * M; r += SY_T) yw[r] = 0.0;
+  for (int r = t; r < M; r += SY_T) v[r] = ws.Vc[(size_t)M * g + r];
   __syncthreads();
-#ifdef OI_SYTRD_TIMING
-  unsigned long long sy_last_ = clock64();
-#endif
-  {
-    const int nb = min(TNB, M - 1 - p);
-    for (int i = 0; i < nb; ++i) {
-      const int g = p + i;
-      // (1) column g with the panel's previous columns: A(r,g) -= V(r,q) W(g,q) + W(r,q) V(g,q)
-      if (i > 0) {
-        // two rows per thread (ra, ra + SY_T), buffer loads: 32 in flight per lane
-        for (int ra = g + t; ra < M; ra += 2 * SY_T) {
-          const int rb = ra + SY_T;
-          const bool okb = rb < M;
-          double sa = A[ra + (size_t)ld * g], sb = okb ? A[rb + (size_t)ld * g] : 0.0;
-#pragma unroll 8
-          for (int q = 0; q < i; ++q) {
-            const double wg = ws.Ws[(size_t)M * q + g], vg = ws.Vc[(size_t)M * (p + q) + g];
-            const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
-            const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
-            sa -= va * wg + wa * vg;
-            sb -= vb * wg + wb * vg;
-          }
-          A[ra + (size_t)ld * g] = sa;
-          if (okb) A[rb + (size_t)ld * g] = sb;
-        }
-        __syncthreads();
-      }
-      SY_STAMP(0);
-      // (2) reflector annihilating A(g+2:M, g) (dlarfg)
-      double xs[1] = {0.0};
-      for (int r = g + 2 + t; r < M; r += SY_T) {
-        const double a = A[r + (size_t)ld * g];
-        xs[0] += a * a;
-      }
-      wg_sum<1>(xs, red);
-      const double alpha = A[g + 1 + (size_t)ld * g];
-      const double xn = sqrt(xs[0]);
-      double tau, beta, scal;
-      if (xn == 0.0) {
-        tau = 0.0;
-        beta = alpha;
-        scal = 0.0;
-      } else {
-        beta = -copysign(sqrt(alpha * alpha + xn * xn), alpha);
-        tau = (beta - alpha) / beta;
-        scal = 1.0 / (alpha - beta);
-      }
-      gdouble* vg = ws.Vc + (size_t)M * g;
-      for (int r = t; r < M; r += SY_T) {
-        const double x = r < g + 1 ? 0.0 : r == g + 1 ? 1.0 : A[r + (size_t)ld * g] * scal;
-        v[r] = x;
-        vg[r] = x;
-      }
-      if (t == 0) {
-        ws.d[g] = A[g + (size_t)ld * g];
-        ws.e[g] = beta;
-        ws.tau[g] = tau;
-      }
-      __syncthreads();
-      SY_STAMP(1);
-      // (3) y = A22 v over the lower triangle of A(g+1:M, g+1:M).  Wave wv owns
-      // groups of SY_C consecutive columns (c0 = g+1 + SY_C (wv + SY_W j)) and
-      // streams their rows in batches of SY_R x 64, so SY_C x SY_R loads per lane
-      // are in flight (one workgroup per matrix: load latency, not bandwidth,
-      // bounds the symv); per row one v[r] read and one yw[wv][r]
-      // read-modify-write (the transposed half) serve the whole group, and the
-      // group's column dots are reduced once at its end
-      double* myw = yw + (size_t)wv * M;
-      for (int c0 = g + 1 + SY_C * wv; c0 < M; c0 += SY_C * SY_W) {
-        const Rsrc rcol = rsrc(E.A + (size_t)ld * c0);
-        double vc[SY_C], dot[SY_C];
+  // (3) y = A22 v over the lower triangle of A(g+1:M, g+1:M): global wave
+  // gw = s SY_W + wv owns the groups of SY_C consecutive columns
+  // c0 = g+1 + SY_C (gw + SY_S SY_W j) and streams their rows in batches of
+  // SY_R x 64; per row one v[r] read and one yw[wv][r] read-modify-write (the
+  // transposed half) serve the whole group; the group's column dots are
+  // reduced once at its end
+  double* myw = yw + (size_t)wv * M;
+  const int gw = sgrp * SY_W + wv;
+  for (int c0 = g + 1 + SY_C * gw; c0 < M; c0 += SY_C * SY_W * SY_S) {
+    const Rsrc rcol = rsrc(E.A + (size_t)ld * c0);
+    double vc[SY_C], dot[SY_C];
+#pragma unroll
+    for (int j = 0; j < SY_C; ++j) {
+      vc[j] = c0 + j < M ? v[c0 + j] : 0.0;
+      dot[j] = 0.0;
+    }
+    for (int r0 = c0; r0 < M; r0 += SY_R * 64) {
+      double a[SY_R][SY_C];
+#pragma unroll
+      for (int u = 0; u < SY_R; ++u)
 #pragma unroll
         for (int j = 0; j < SY_C; ++j) {
-          vc[j] = c0 + j < M ? v[c0 + j] : 0.0;
-          dot[j] = 0.0;
+          const int r = r0 + lane + 64 * u;
+          a[u][j] = bload(rcol, r < M && r >= c0 + j, r + (size_t)ld * j);
         }
-        for (int r0 = c0; r0 < M; r0 += SY_R * 64) {
-          double a[SY_R][SY_C];
 #pragma unroll
-          for (int u = 0; u < SY_R; ++u)
+      for (int u = 0; u < SY_R; ++u) {
+        const int r = r0 + lane + 64 * u;
+        if (r < M) {
+          const double vr = v[r];
+          double tr = 0.0;
 #pragma unroll
-            for (int j = 0; j < SY_C; ++j) {
-              // unconditional loads from clamped addresses (a branch per load
-              // would serialise them), masked afterwards
-              const int r = r0 + lane + 64 * u;
-              a[u][j] = bload(rcol, r < M && r >= c0 + j, r + (size_t)ld * j);
-            }
-#pragma unroll
-          for (int u = 0; u < SY_R; ++u) {
-            const int r = r0 + lane + 64 * u;
-            if (r < M) {
-              const double vr = v[r];
-              double tr = 0.0;
-#pragma unroll
-              for (int j = 0; j < SY_C; ++j) {
-                dot[j] += a[u][j] * vr;
-                if (r > c0 + j) tr += a[u][j] * vc[j];
-              }
-              myw[r] += tr;
-            }
+          for (int j = 0; j < SY_C; ++j) {
+            dot[j] += a[u][j] * vr;
+            if (r > c0 + j) tr += a[u][j] * vc[j];
           }
-        }
-#pragma unroll
-        for (int j = 0; j < SY_C; ++j)
-          for (int o = 32; o > 0; o >>= 1) dot[j] += __shfl_down(dot[j], o, 64);
-        if (lane == 0)
-#pragma unroll
-          for (int j = 0; j < SY_C; ++j)
-            if (c0 + j < M) myw[c0 + j] += dot[j];
-      }
-      SY_STAMP(2);
-      // panel corrections: pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g)
-      // (4 dots per wave at a time, 4 row chunks each: 16 loads per lane in flight)
-      for (int jq0 = 4 * wv; jq0 < 2 * i; jq0 += 4 * SY_W) {
-        const gdouble* col[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int jq = min(jq0 + d, 2 * i - 1), q = jq % i;
-          col[d] = jq < i ? ws.Ws + (size_t)M * q : ws.Vc + (size_t)M * (p + q);
-        }
-        double s4[4][4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) s4[d][u] = 0.0;
-        for (int r = g + 1 + lane; r < M; r += 256) {
-          double a[4][4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              const double x = col[d][min(r + 64 * u, M - 1)];
-              a[d][u] = r + 64 * u < M ? x : 0.0;
-            }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const double vr = r + 64 * u < M ? v[min(r + 64 * u, M - 1)] : 0.0;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) s4[d][u] += a[d][u] * vr;
-          }
-        }
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          double s = (s4[d][0] + s4[d][1]) + (s4[d][2] + s4[d][3]);
-          for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-          const int jq = jq0 + d;
-          if (lane == 0 && jq < 2 * i) pan[(jq < i ? 0 : TNB) + jq % i] = s;
+          myw[r] += tr;
         }
       }
-      __syncthreads();
-      SY_STAMP(3);
-      // column i of the block reflector's T (dlarft, forward columnwise):
-      // T(i,i) = tau, T(a,i) = -tau sum_{a<=k<i} T(a,k) (V_k'v), V_k'v = pan[TNB + k]
-      if (t <= i) {
-        double x = tau;
-        if (t < i) {
-          x = 0.0;
-          for (int k = t; k < i; ++k) x += Tl[t + TNB * k] * pan[TNB + k];
-          x *= -tau;
-        }
-        Tl[t + TNB * i] = x;
-      }
-      // (4) w = tau (y - V (W'v) - W (V'v)), then w += -tau/2 (w'v) v
-      double sv[1] = {0.0};
-      for (int ra = g + 1 + t; ra < M; ra += 2 * SY_T) {
-        const int rb = ra + SY_T;
-        const bool okb = rb < M;
-        double sa = 0.0, sb = 0.0;
+    }
 #pragma unroll
-        for (int ww = 0; ww < SY_W; ++ww) {
-          sa += yw[(size_t)ww * M + ra];
-          yw[(size_t)ww * M + ra] = 0.0;
-          if (okb) {
-            sb += yw[(size_t)ww * M + rb];
-            yw[(size_t)ww * M + rb] = 0.0;
-          }
-        }
+    for (int j = 0; j < SY_C; ++j)
+      for (int o = 32; o > 0; o >>= 1) dot[j] += __shfl_down(dot[j], o, 64);
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < SY_C; ++j)
+        if (c0 + j < M) myw[c0 + j] += dot[j];
+  }
+  // panel dots, one per global wave (rows > g, 4 row chunks per load batch)
+  for (int jq = gw; jq < 2 * i; jq += SY_W * SY_S) {
+    const int q = jq % i;
+    const Rsrc rc = rsrc(jq < i ? carve(E.work, M).Ws + (size_t)M * q : carve(E.work, M).Vc + (size_t)M * (p + q));
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int r = g + 1 + lane; r < M; r += 256) {
+      double a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = bload(rc, r + 64 * u < M, r + 64 * u);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r + 64 * u < M) s4[u] += a[u] * v[r + 64 * u];
+    }
+    double sd = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    for (int o = 32; o > 0; o >>= 1) sd += __shfl_down(sd, o, 64);
+    if (lane == 0) ws.X[(jq < i ? 0 : TNB) + q] = sd;
+  }
+  __syncthreads();
+  gdouble* yp = ws.H + (size_t)sgrp * M;
+  for (int r = g + 1 + t; r < M; r += SY_T) {
+    double sy = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < SY_W; ++ww) sy += yw[(size_t)ww * M + r];
+    yp[r] = sy;
+  }
+}
+
+__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i) {
+  __shared__ double red[64];
+  __shared__ double pan[2 * TNB];
+  const Eigh E = es[blockIdx.x];
+  const int M = E.M, t = threadIdx.x, g = p + i;
+  if (g >= M - 1) return;
+  EighWsG ws = carveG(E.work, M);
+  const Rsrc rV = rsrc(carve(E.work, M).Vc + (size_t)M * p), rW = rsrc(carve(E.work, M).Ws);
+  const double tau = ws.tau[g];
+  if (t < 2 * TNB) pan[t] = t % TNB < i ? ws.X[t] : 0.0;
+  // column i of the block reflector's T (dlarft, forward columnwise), in the
+  // workspace: T(i,i) = tau, T(a,i) = -tau sum_{a<=k<i} T(a,k) (V_k'v)
+  gdouble* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
+  if (i == 0)
+    for (int e = t; e < TNB * TNB; e += SY_T) Tp[e] = 0.0;
+  __syncthreads();
+  if (t <= i) {
+    double x = tau;
+    if (t < i) {
+      x = 0.0;
+      for (int k = t; k < i; ++k) x += Tp[t + TNB * k] * pan[TNB + k];
+      x *= -tau;
+    }
+    Tp[t + TNB * i] = x;
+  }
+  // (4) w = tau (y - V (W'v) - W (V'v)), y = sum of the SY_S partials; then
+  // w += -tau/2 (w'v) v; two rows per thread
+  const gdouble* vgc = ws.Vc + (size_t)M * g;
+  double sv[1] = {0.0};
+  double wr2[2][4];  // rows ra, rb of each sweep (M <= 4096: at most 4 sweeps)
+  int nsw = 0;
+  for (int ra = g + 1 + t; ra < M; ra += 2 * SY_T, ++nsw) {
+    const int rb = ra + SY_T;
+    const bool okb = rb < M;
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int s = 0; s < SY_S; ++s) {
+      sa += ws.H[(size_t)s * M + ra];
+      if (okb) sb += ws.H[(size_t)s * M + rb];
+    }
 #pragma unroll 8
-        for (int q = 0; q < i; ++q) {
-          const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
-          const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
-          sa -= va * pan[q] + wa * pan[TNB + q];
-          sb -= vb * pan[q] + wb * pan[TNB + q];
-        }
-        const double wra = tau * sa;
-        y[ra] = wra;
-        sv[0] += wra * v[ra];
-        if (okb) {
-          const double wrb = tau * sb;
-          y[rb] = wrb;
-          sv[0] += wrb * v[rb];
-        }
-      }
-      wg_sum<1>(sv, red);
-      const double a2 = -0.5 * tau * sv[0];
-      gdouble* wcol = ws.Ws + (size_t)M * i;
-      for (int r = t; r < M; r += SY_T) wcol[r] = r <= g ? 0.0 : y[r] + a2 * v[r];
-      __syncthreads();
+    for (int q = 0; q < i; ++q) {
+      const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
+      const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
+      sa -= va * pan[q] + wa * pan[TNB + q];
+      sb -= vb * pan[q] + wb * pan[TNB + q];
     }
-    SY_STAMP(4);
-    // T of the block reflector H_p ... H_{p+nb-1} = I - V T V' (formed column
-    // by column in step (4)) to the workspace for the back-transform
-    gdouble* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
-    for (int e = t; e < TNB * TNB; e += SY_T) {
-      Tp[e] = Tl[e];
-      Tl[e] = 0.0;
+    const double wra = tau * sa;
+    sv[0] += wra * vgc[ra];
+    double wrb = 0.0;
+    if (okb) {
+      wrb = tau * sb;
+      sv[0] += wrb * vgc[rb];
     }
-    SY_STAMP(5);
+    if (nsw < 4) {
+      wr2[0][nsw] = wra;
+      wr2[1][nsw] = wrb;
+    }
+  }
+  wg_sum<1>(sv, red);
+  const double a2 = -0.5 * tau * sv[0];
+  gdouble* wcol = ws.Ws + (size_t)M * i;
+  for (int r = t; r <= g && r < M; r += SY_T) wcol[r] = 0.0;
+  nsw = 0;
+  for (int ra = g + 1 + t; ra < M; ra += 2 * SY_T, ++nsw) {
+    const int rb = ra + SY_T;
+    if (nsw < 4) {
+      wcol[ra] = wr2[0][nsw] + a2 * vgc[ra];
+      if (rb < M) wcol[rb] = wr2[1][nsw] + a2 * vgc[rb];
+    }
   }
 }
 
@@ -1145,14 +1129,18 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   if (Mmax > 4096) throw LinalgErr{"eigh: M > 4096 not supported"};
   const Eigh* de = S.put(es);
   const unsigned n = (unsigned)es.size();
-  const size_t lds_sy = ((size_t)(SY_W + 2) * Mmax + 64 + 2 * TNB + TNB * TNB) * sizeof(double);
+  const size_t lds_sy = (size_t)(SY_W + 1) * Mmax * sizeof(double);
   if (lds_sy > 160 * 1024) throw LinalgErr{"eigh: matrix too large for the tridiagonalisation's LDS"};
   phase(0);
   // panel by panel: the panel's 32 reflectors on one workgroup per matrix,
   // then its trailing update A22 -= V W' + W V' (lower 64 x 64 tiles) as two
   // batched GEMMs over the whole chip
   for (int p = 0; p < std::max(Mmax - 1, 1); p += TNB) {
-    hipLaunchKernelGGL(k_sytrd_panel, dim3(n), dim3(SY_T), lds_sy, st, de, p);
+    for (int i = 0; i < TNB && (i == 0 || p + i < Mmax - 1); ++i) {
+      hipLaunchKernelGGL(k_sy_reflect, dim3(n), dim3(SY_T), 0, st, de, p, i);
+      hipLaunchKernelGGL(k_sy_symv, dim3(n, SY_S), dim3(SY_T), lds_sy, st, de, p, i);
+      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i);
+    }
     LC(hipGetLastError());
     std::vector<Gemm> g1, g2;
     for (const Eigh& e : es) {

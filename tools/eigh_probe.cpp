@@ -1,6 +1,5 @@
 // Phase times of oila::eigh on a chunk of Matern K_mm matrices (the Nystrom
-// variant's M = 925 padded to 928, 32 per chunk), plus the per-phase cycle
-// split of k_sytrd on matrix 0 (build: see tools/build_eigh_probe.sh).
+// variant's M = 925 padded to 928, 32 per chunk) (build: tools/build_eigh_probe.sh).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -11,7 +10,6 @@
 
 #include "../optimalinterpolation_amd/csrc/oi_linalg.h"
 
-extern "C" int oila_sytrd_cycles(unsigned long long* out);
 
 #define CK(x)                                                             \
   do {                                                                    \
@@ -72,14 +70,6 @@ int main(int argc, char** argv) {
   }
   printf("eigh M=%d x %d: sytrd %.2f ms, stebz+stein %.2f ms, orth %.2f ms, back %.2f ms\n", M, nb, ph[0],
          ph[1], ph[2], ph[3]);
-  unsigned long long cyc[8];
-  if (oila_sytrd_cycles(cyc) == 0) {
-    const char* nm[7] = {"col update", "dlarfg", "symv", "panel gemv", "w + T col", "T store", "trailing"};
-    double tot = 0;
-    for (int k = 0; k < 7; ++k) tot += cyc[k];
-    for (int k = 0; k < 7; ++k) printf("  sytrd %-10s %5.1f %%  (%.2f Mcycles per call)\n", nm[k], 100.0 * cyc[k] / tot,
-                                       cyc[k] / 1e6 / (reps + 1));
-  }
   std::vector<double> wh((size_t)M * nb);
   CK(hipMemcpy(wh.data(), w, wh.size() * 8, hipMemcpyDeviceToHost));
   printf("eigenvalues of matrix 0: min %.3e max %.3e\n", wh[0], wh[M - 1]);
