@@ -491,7 +491,7 @@ def main_nystrom(args, torch, dist, world, rank, gpu, cdev):
                     outs[k] = sess.wait(tickets[k])
         return [outs[k] for k in ks]
 
-    if not args.no_prime:  # library / rocBLAS / rocSOLVER initialisation, not a step
+    if not args.no_prime:  # library / code-object initialisation, not a step
         pc = synthetic.make_cells([300], seed=4321)
         ps, po = nystrom._ragged_sel(pc.offs, 60)
         _lib.nystrom_fit_batch(pc.xyt, pc.z - pc.mean, pc.offs, ps, po, x0, pc.xs, pc.mean, device=gpu)

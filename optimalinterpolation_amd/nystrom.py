@@ -16,7 +16,8 @@ cell 5) fits and predicts with:
 * ``*_batch`` forms take ragged cells (xyt, y, offs) and run one liboi call.
 
 The approx=True arithmetic runs on the GPU (liboi ``oi_nystrom_batch``:
-rocSOLVER eigh / Cholesky, rocBLAS panels, fused HIP objective pass); the
+hand-written batched eigensolver, blocked Cholesky and MFMA products of
+csrc/oi_linalg.hip, fused HIP objective pass; no vendor BLAS / LAPACK); the
 approx=False branch is the full GP of the main path (``oi_nlml_grad_batch`` /
 ``oi_gpr_batch``).  Only the inducing-row draw is host-side, exactly NB1's.
 """
