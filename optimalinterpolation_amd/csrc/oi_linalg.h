@@ -87,8 +87,6 @@ class Stager {
     return static_cast<const T*>(put_bytes(v.data(), v.size() * sizeof(T)));
   }
   void reset() { off_ = 0; }
-  // device scratch on this stream (grown as needed; valid until the next call)
-  double* scratch(size_t doubles);
 
  private:
   const void* put_bytes(const void* p, size_t bytes);
@@ -96,8 +94,6 @@ class Stager {
   char* host_ = nullptr;
   char* dev_ = nullptr;
   size_t cap_ = 0, off_ = 0;
-  double* scr_ = nullptr;
-  size_t scap_ = 0;
   std::vector<std::pair<char*, char*>> retired_;  // grown-out buffers, freed at destruction
 };
 

@@ -88,11 +88,8 @@ __device__ __forceinline__ double bload(Rsrc r, bool ok, size_t idx) {
 #define GKC 16
 #define GLD 80  // LDS row stride of a staged 16 x 64 chunk (rows k, k+1 in opposite bank halves)
 
-// Split-k (ksplit > 1, blockIdx.z = the slice): each workgroup sums its
-// slice of the k chunks and writes the raw 64 x 64 tile to part; then
-// k_gemm_reduce adds the slices in a fixed order and applies alpha / beta.
 template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs, int ksplit, double* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
   __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GKC * GLD];
   const Gemm g = gs[blockIdx.y];
   const int tm = (g.m + GT - 1) / GT, tn = (g.n + GT - 1) / GT;
@@ -149,15 +146,14 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs, int k
       acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
     }
   };
-  const int cps = (nch + ksplit - 1) / ksplit, cbeg = (int)blockIdx.z * cps, cend = min(nch, cbeg + cps);
-  if (cend > cbeg) {
-    load(cbeg);
+  if (nch > 0) {
+    load(0);
     store(0);
     __syncthreads();
-    for (int ch = cbeg; ch < cend; ++ch) {
-      if (ch + 1 < cend) load(ch + 1);
-      compute((ch - cbeg) & 1);
-      if (ch + 1 < cend) store((ch - cbeg + 1) & 1);
+    for (int ch = 0; ch < nch; ++ch) {
+      if (ch + 1 < nch) load(ch + 1);
+      compute(ch & 1);
+      if (ch + 1 < nch) store((ch + 1) & 1);
       __syncthreads();
     }
   }
@@ -170,36 +166,11 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs, int k
 #pragma unroll
       for (int r = 0; r < 4; ++r) X[acc1_col(nb) * 65 + acc1_row(mb, r)] = acc.c[mb][nb][r];
   __syncthreads();
-  if (ksplit > 1) {
-    gdouble* P = G(part) + (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (GT * GT);
-    for (int e = t; e < GT * GT; e += 256) P[e] = X[(e >> 6) * 65 + (e & 63)];
-    return;
-  }
   for (int e = t; e < GT * GT; e += 256) {
     const int m = e & 63, n = e >> 6, gm = m0 + m, gn = n0 + n;
     if (gm >= g.m || gn >= g.n) continue;
     gdouble* c = G(g.C) + gm + (size_t)g.ldc * gn;
     const double v = g.alpha * X[n * 65 + m];
-    *c = g.beta == 0.0 ? v : v + g.beta * *c;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_gemm_reduce(const Gemm* __restrict__ gs, int ksplit,
-                                                     const double* __restrict__ part) {
-  const Gemm g = gs[blockIdx.y];
-  const int tm = (g.m + GT - 1) / GT, tn = (g.n + GT - 1) / GT;
-  if ((int)blockIdx.x >= tm * tn) return;
-  const int it = blockIdx.x % tm, jt = blockIdx.x / tm;
-  if (g.tri == 1 && it < jt) return;
-  const size_t slice = (size_t)gridDim.y * gridDim.x * (GT * GT);
-  const gdouble* P = G(part) + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (GT * GT);
-  for (int e = threadIdx.x; e < GT * GT; e += 256) {
-    const int m = e & 63, n = e >> 6, gm = GT * it + m, gn = GT * jt + n;
-    if (gm >= g.m || gn >= g.n) continue;
-    double sum = P[n * GT + m];
-    for (int z = 1; z < ksplit; ++z) sum += P[z * slice + n * GT + m];
-    gdouble* c = G(g.C) + gm + (size_t)g.ldc * gn;
-    const double v = g.alpha * sum;
     *c = g.beta == 0.0 ? v : v + g.beta * *c;
   }
 }
@@ -357,10 +328,15 @@ __device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] =
 //                       - tau/2 (w'v) v, column i of the panel's T (dlarft)
 // then, per panel, the trailing update A22 -= V W' + W V' on oila::gemm.
 #define SY_S 8  // symv workgroups per matrix
-// column g = p + i: update with the panel's earlier reflectors, reflector
-// (the caller has checked g < M - 1)
-__device__ __forceinline__ void sy_reflect(const Eigh& E, int p, int i, double* red) {
+__global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es, int p, int i) {
+  __shared__ double red[64];
+  const Eigh E = es[blockIdx.x];
   const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i;
+  if (p >= M - 1) {
+    if (p == 0 && i == 0 && t == 0) ws_d0(E);  // M == 1
+    return;
+  }
+  if (g >= M - 1) return;  // this matrix's last panel is shorter
   gdouble* A = G(E.A);
   EighWsG ws = carveG(E.work, M);
   const Rsrc rV = rsrc(carve(E.work, M).Vc + (size_t)M * p), rW = rsrc(carve(E.work, M).Ws);  // panel V, W
@@ -409,17 +385,6 @@ __device__ __forceinline__ void sy_reflect(const Eigh& E, int p, int i, double* 
     ws.e[g] = beta;
     ws.tau[g] = tau;
   }
-}
-__global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es, int p, int i) {
-  __shared__ double red[64];
-  const Eigh E = es[blockIdx.x];
-  const int M = E.M;
-  if (p >= M - 1) {
-    if (p == 0 && i == 0 && threadIdx.x == 0) ws_d0(E);  // M == 1
-    return;
-  }
-  if (p + i >= M - 1) return;  // this matrix's last panel is shorter
-  sy_reflect(E, p, i, red);
 }
 
 // partial y of workgroup s into H[s M + r] (rows g+1 .. M-1); the panel dots
@@ -511,7 +476,7 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
   }
 }
 
-__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i, int fuse_next) {
+__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i) {
   __shared__ double red[64];
   __shared__ double pan[2 * TNB];
   const Eigh E = es[blockIdx.x];
@@ -581,11 +546,6 @@ __global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int 
       wcol[ra] = wr2[0][nsw] + a2 * vgc[ra];
       if (rb < M) wcol[rb] = wr2[1][nsw] + a2 * vgc[rb];
     }
-  }
-  // the next column of the panel in the same launch (saves one launch per column)
-  if (fuse_next && i + 1 < TNB && g + 1 < M - 1) {
-    __syncthreads();  // W(:, i) complete (workgroup-scope: global stores visible)
-    sy_reflect(E, p, i + 1, red);
   }
 }
 
@@ -930,9 +890,8 @@ __global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es,
 #define RL (TNB + 1)  // LDS row stride of R and R^-1
 __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es, int p) {
   __shared__ double Gw[MG_T / 64][TNB * TNB];
-  __shared__ double R[TNB * RL];   // G, then the trailing updates of the factorisation
-  __shared__ double Rs[TNB * RL];  // the factor R (upper; identity beyond nb)
-  __shared__ double Ri[TNB * RL];  // R^-1
+  __shared__ double R[TNB * RL];
+  __shared__ double Ri[TNB * RL];
   __shared__ double gd[TNB];
   __shared__ int bad;
   const Eigh E = es[blockIdx.x];
@@ -944,31 +903,25 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
   gdouble* Z = G(E.A) + ld * p;
   const Rsrc rz = rsrc(E.A + ld * p);
   if (t == 0) carve(E.work, M).flag[0] = 0.0;
-  constexpr int NW = MG_T / 64, RB = 4;  // waves; 16-row blocks per load batch
   for (int pass = 0; pass < 2; ++pass) {
-    // (1) G = Z_p' Z_p: wave w sums the 16-row blocks w + NW j, RB blocks (4 k-steps
-    // each) per load batch
+    // (1) G = Z_p' Z_p: wave w sums the 16-row blocks 16 (w + 4 j), 4 k-steps per batch
     Quad acc;
     quad_zero(acc);
-    for (int i0 = 16 * w; i0 < M; i0 += 16 * NW * RB) {
-      double a0[RB][4], a1[RB][4];
+    for (int i0 = 16 * w; i0 < M; i0 += 16 * (MG_T / 64)) {
+      double a0[4], a1[4];
 #pragma unroll
-      for (int b = 0; b < RB; ++b)
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 4 * u + fk;
+        a0[u] = bload(rz, i < M && fr < nb, i + ld * fr);
+        a1[u] = bload(rz, i < M && 16 + fr < nb, i + ld * (16 + fr));
+      }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = i0 + 16 * NW * b + 4 * u + fk;
-          a0[b][u] = bload(rz, i < M && fr < nb, i + ld * fr);
-          a1[b][u] = bload(rz, i < M && 16 + fr < nb, i + ld * (16 + fr));
-        }
-#pragma unroll
-      for (int b = 0; b < RB; ++b)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc.c[0][0] = MFMA64(a0[b][u], a0[b][u], acc.c[0][0]);
-          acc.c[0][1] = MFMA64(a0[b][u], a1[b][u], acc.c[0][1]);
-          acc.c[1][0] = MFMA64(a1[b][u], a0[b][u], acc.c[1][0]);
-          acc.c[1][1] = MFMA64(a1[b][u], a1[b][u], acc.c[1][1]);
-        }
+      for (int u = 0; u < 4; ++u) {
+        acc.c[0][0] = MFMA64(a0[u], a0[u], acc.c[0][0]);
+        acc.c[0][1] = MFMA64(a0[u], a1[u], acc.c[0][1]);
+        acc.c[1][0] = MFMA64(a1[u], a0[u], acc.c[1][0]);
+        acc.c[1][1] = MFMA64(a1[u], a1[u], acc.c[1][1]);
+      }
     }
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
@@ -984,25 +937,27 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
       double g = 0.0;
       if (a <= b && b < nb) {
         g = Gw[0][e];
-        for (int ww = 1; ww < NW; ++ww) g += Gw[ww][e];
+        for (int ww = 1; ww < MG_T / 64; ++ww) g += Gw[ww][e];
       }
       R[a + RL * b] = g;
-      Rs[a + RL * b] = a == b && b >= nb ? 1.0 : 0.0;
       if (a == b) gd[a] = g;
     }
     __syncthreads();
-    // (2) G = R'R, right-looking, one barrier per column: every thread forms
-    // the pivot itself; row j of the factor goes to Rs, the trailing update
-    // A(a,b) -= R(j,a) R(j,b) (unscaled) / d_j stays in R
+    // (2) G = R'R (upper R, right-looking, row j scaled by its pivot)
     for (int j = 0; j < nb; ++j) {
-      const double dj = R[j + RL * j];
-      const double rj = sqrt(fmax(dj, 1e-300)), id = 1.0 / fmax(dj, 1e-300);
-      if (t == 0 && !(dj > 1e-4 * gd[j])) bad = 1;
+      if (t == 0) {
+        const double dj = R[j + RL * j];
+        if (!(dj > 1e-4 * gd[j])) bad = 1;
+        R[j + RL * j] = sqrt(fmax(dj, 1e-300));
+      }
+      __syncthreads();
+      const double inv = 1.0 / R[j + RL * j];
+      for (int l = j + 1 + t; l < nb; l += MG_T) R[j + RL * l] *= inv;
+      __syncthreads();
       const int L = nb - j - 1;
-      if (t <= L) Rs[j + RL * (j + t)] = t == 0 ? rj : R[j + RL * (j + t)] / rj;
       for (int e = t; e < L * L; e += MG_T) {
         const int a = j + 1 + e % L, b = j + 1 + e / L;
-        if (a <= b) R[a + RL * b] -= (R[j + RL * a] * R[j + RL * b]) * id;
+        if (a <= b) R[a + RL * b] -= R[j + RL * a] * R[j + RL * b];
       }
       __syncthreads();
     }
@@ -1010,68 +965,45 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
       if (t == 0) carve(E.work, M).flag[0] = 1.0;
       return;
     }
-    // (3) R^-1 by 16 x 16 blocks: the diagonal blocks by back substitution, one
-    // thread per column (both blocks at once), then Ri12 = -Ri11 (R12 Ri22)
+    // (3) R^-1 (upper), one thread per column
     if (t < TNB) {
-      const int l = t, o = l < 16 ? 0 : 16;
-      for (int a = o + 15; a >= o; --a) {
+      const int l = t;
+      for (int a = TNB - 1; a >= 0; --a) {
         double x = 0.0;
-        if (a <= l) {
+        if (l < nb && a <= l) {
           x = a == l ? 1.0 : 0.0;
-          for (int k = a + 1; k <= l; ++k) x -= Rs[a + RL * k] * Ri[k + RL * l];
-          x /= Rs[a + RL * a];
+          for (int k = a + 1; k <= l; ++k) x -= R[a + RL * k] * Ri[k + RL * l];
+          x /= R[a + RL * a];
         }
         Ri[a + RL * l] = x;
       }
-      for (int a = 16; a < TNB; ++a)
-        if (l < 16) Ri[a + RL * l] = 0.0;
     }
     __syncthreads();
-    double* X = Gw[0];  // R12 Ri22 (16 x 16)
-    {
-      const int a = t & 15, c = t >> 4;  // 256 threads: one element each
-      double x = 0.0;
-      for (int k = 0; k <= c; ++k) x += Rs[a + RL * (16 + k)] * Ri[(16 + k) + RL * (16 + c)];
-      X[a + 16 * c] = x;
-    }
-    __syncthreads();
-    {
-      const int a = t & 15, c = t >> 4;
-      double x = 0.0;
-      for (int k = a; k < 16; ++k) x += Ri[a + RL * k] * X[k + 16 * c];
-      Ri[a + RL * (16 + c)] = -x;
-    }
-    __syncthreads();
-    // (4) Z_p <- Z_p R^-1 on the MFMA core, wave w over the 16-row blocks w + NW j, two per batch
+    // (4) Z_p <- Z_p R^-1 on the MFMA core, wave w over the 16-row blocks 16 (w + 4 j)
     double rb[2][TNB / 4];
 #pragma unroll
     for (int kk = 0; kk < TNB / 4; ++kk)
 #pragma unroll
       for (int nbk = 0; nbk < 2; ++nbk) rb[nbk][kk] = Ri[(4 * kk + fk) + RL * (16 * nbk + fr)];
-    for (int i0 = 16 * w; i0 < M; i0 += 16 * NW * 2) {
-      double za[2][TNB / 4];
+    for (int i0 = 16 * w; i0 < M; i0 += 16 * (MG_T / 64)) {
+      double za[TNB / 4];
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int kk = 0; kk < TNB / 4; ++kk) {
+        const int i = i0 + fr, a = 4 * kk + fk;
+        za[kk] = bload(rz, i < M && a < nb, i + ld * a);
+      }
+      d4 o0 = (d4){0.0, 0.0, 0.0, 0.0}, o1 = o0;
 #pragma unroll
-        for (int kk = 0; kk < TNB / 4; ++kk) {
-          const int i = i0 + 16 * NW * b + fr, a = 4 * kk + fk;
-          za[b][kk] = bload(rz, i < M && a < nb, i + ld * a);
-        }
+      for (int kk = 0; kk < TNB / 4; ++kk) {
+        o0 = MFMA64(za[kk], rb[0][kk], o0);
+        o1 = MFMA64(za[kk], rb[1][kk], o1);
+      }
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        d4 o0 = (d4){0.0, 0.0, 0.0, 0.0}, o1 = o0;
-#pragma unroll
-        for (int kk = 0; kk < TNB / 4; ++kk) {
-          o0 = MFMA64(za[b][kk], rb[0][kk], o0);
-          o1 = MFMA64(za[b][kk], rb[1][kk], o1);
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int i = i0 + 16 * NW * b + (lane >> 4) + 4 * rr, c = lane & 15;
-          if (i < M) {
-            if (c < nb) Z[i + ld * c] = o0[rr];
-            if (16 + c < nb) Z[i + ld * (16 + c)] = o1[rr];
-          }
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = i0 + (lane >> 4) + 4 * rr, c = lane & 15;
+        if (i < M) {
+          if (c < nb) Z[i + ld * c] = o0[rr];
+          if (16 + c < nb) Z[i + ld * (16 + c)] = o1[rr];
         }
       }
     }
@@ -1083,20 +1015,10 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
 Stager::~Stager() {
   if (host_) (void)hipHostFree(host_);
   if (dev_) (void)hipFree(dev_);
-  if (scr_) (void)hipFree(scr_);
   for (auto& pr : retired_) {
-    if (pr.first) (void)hipHostFree(pr.first);
+    (void)hipHostFree(pr.first);
     (void)hipFree(pr.second);
   }
-}
-
-double* Stager::scratch(size_t doubles) {
-  if (doubles > scap_) {
-    if (scr_) retired_.push_back({nullptr, (char*)scr_});  // may still be in use by queued launches
-    LC(hipMalloc((void**)&scr_, doubles * sizeof(double)));
-    scap_ = doubles;
-  }
-  return scr_;
 }
 
 const void* Stager::put_bytes(const void* p, size_t bytes) {
@@ -1127,25 +1049,12 @@ void gemm(Stager& S, hipStream_t st, bool ta, bool tb, const std::vector<Gemm>& 
     }
   if (live.empty()) return;
   const Gemm* dg = S.put(live);
-  // split k when the batch has too few output tiles to fill the chip and each
-  // slice keeps >= 8 chunks of 16 (the eigensolver's tall-skinny products)
-  int kmax = 0;
-  for (const Gemm& x : live) kmax = std::max(kmax, x.k);
-  const long wgs = (long)tiles * (long)live.size();
-  int ksplit = 1;
-  while (ksplit < 8 && wgs * ksplit * 2 <= 1024 && kmax / (ksplit * 2) >= 8 * GKC) ksplit *= 2;
-  double* part = ksplit > 1 ? S.scratch((size_t)ksplit * wgs * GT * GT) : nullptr;
-  dim3 grid((unsigned)tiles, (unsigned)live.size(), (unsigned)ksplit);
-  if (ta && tb) hipLaunchKernelGGL((k_gemm<true, true>), grid, dim3(256), 0, st, dg, ksplit, part);
-  else if (ta) hipLaunchKernelGGL((k_gemm<true, false>), grid, dim3(256), 0, st, dg, ksplit, part);
-  else if (tb) hipLaunchKernelGGL((k_gemm<false, true>), grid, dim3(256), 0, st, dg, ksplit, part);
-  else hipLaunchKernelGGL((k_gemm<false, false>), grid, dim3(256), 0, st, dg, ksplit, part);
+  dim3 grid((unsigned)tiles, (unsigned)live.size());
+  if (ta && tb) hipLaunchKernelGGL((k_gemm<true, true>), grid, dim3(256), 0, st, dg);
+  else if (ta) hipLaunchKernelGGL((k_gemm<true, false>), grid, dim3(256), 0, st, dg);
+  else if (tb) hipLaunchKernelGGL((k_gemm<false, true>), grid, dim3(256), 0, st, dg);
+  else hipLaunchKernelGGL((k_gemm<false, false>), grid, dim3(256), 0, st, dg);
   LC(hipGetLastError());
-  if (ksplit > 1) {
-    hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)tiles, (unsigned)live.size()), dim3(256), 0, st, dg, ksplit,
-                       (const double*)part);
-    LC(hipGetLastError());
-  }
 }
 
 void gemv(Stager& S, hipStream_t st, bool trans, const std::vector<Gemv>& g) {
@@ -1228,10 +1137,9 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   // batched GEMMs over the whole chip
   for (int p = 0; p < std::max(Mmax - 1, 1); p += TNB) {
     for (int i = 0; i < TNB && (i == 0 || p + i < Mmax - 1); ++i) {
-      // the panel's first reflector has a launch of its own; k_sy_w(i) forms the next one
-      if (i == 0) hipLaunchKernelGGL(k_sy_reflect, dim3(n), dim3(SY_T), 0, st, de, p, i);
+      hipLaunchKernelGGL(k_sy_reflect, dim3(n), dim3(SY_T), 0, st, de, p, i);
       hipLaunchKernelGGL(k_sy_symv, dim3(n, SY_S), dim3(SY_T), lds_sy, st, de, p, i);
-      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i, 1);
+      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i);
     }
     LC(hipGetLastError());
     std::vector<Gemm> g1, g2;
