@@ -72,7 +72,10 @@ def parse():
     p.add_argument('--slices', default='ordered', choices=['lpt', 'ordered'],
                    help='day slices: equal-cost LPT mixes (lpt) or consecutive runs of the '
                         'largest-n-first order (ordered)')
-    p.add_argument('--depth', type=int, default=8, help='slices in flight beyond the one waited on')
+    p.add_argument('--depth', type=int, default=None,
+                   help='slices in flight beyond the one waited on (default: 8 for a whole day on one GPU; '
+                        'every slice for a rank share of the day, config 4 -- profiles/r04/day_share_8of8.json; '
+                        '8 for nystrom)')
     p.add_argument('--pregathered', action='store_true',
                    help='day / season: submit each slice from pre-gathered per-cell inputs (round 2) instead of '
                         'the radius query + gather over the pooled training set inside the timed region')
@@ -412,6 +415,7 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline):
             "e_gpu_small": round(float(np.mean(gpu_evals[small])), 2) if small.any() else None,
             "fit_time_model_k": round(k, 4),
             "fit_time_residual_max_abs": round(float(np.max(np.abs(resid))), 4),
+            "fit_time_total_residual": round(float(np.sum(k * model) / np.sum(meas) - 1.0), 4),
             "fit_time_residuals": [round(float(r), 4) for r in resid],
             "probe_s": {str(kk): [round(v[0], 5), round(v[1], 5)] for kk, v in med.items()},
             "cpu_s_per_cell_mean": round(float(np.mean(t_cells)), 3)}
@@ -809,12 +813,21 @@ def main():
     dev = torch.device('cuda', gpu)
     cdev = torch.device('cpu') if backend == 'gloo' else dev  # where collective tensors live
     if args.workload == 'nystrom':
+        if args.depth is None:
+            args.depth = 8
         return main_nystrom(args, torch, dist, world, rank, gpu, cdev)
     if args.workload == 'svgp':
         return main_svgp(args, torch, dist, world, rank, gpu, cdev)
     from optimalinterpolation_amd import _lib, synthetic
 
     slices, warm, opt, cfg, scaling, counts_all = build_slices(args, rank, world)
+    if args.depth is None:
+        # a rank's share of the day (config 4: ~1250 cells in 20 slices of ~62) goes in all at once,
+        # so the session's rounds stay near the 1-GPU resident size (8 shares at depth 20 on one GPU:
+        # 0.90 projected efficiency, profiles/r04/day_share_8of8.json); a whole day on one GPU keeps
+        # 8 slices in flight
+        args.depth = 8 if (world == 1 and not args.day_shares) else max(1, len(slices))
+    cfg["depth"] = args.depth
     x0 = X0_12P5 if args.workload == 'season' else X0
     log(f"rank {rank}: {len(slices)} slices, {sum(s.ncell for s in slices)} cells")
 
