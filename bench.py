@@ -31,8 +31,13 @@ line then says `"truncated": true` with the slices actually timed.  The CPU
 baseline runs after the GPU leg (rank 0, N = 1) inside the remaining budget.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-                       [--workload day|days|predict|single|nystrom|svgp]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+                       [--workload day|days|season|predict|single|nystrom|svgp]
+Multi-GPU: `python bench.py --gpus N` starts N rank processes itself (one per
+GPU, torch.distributed over RCCL; launch_ranks below) before anything touches
+the GPU, or run it under `python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N` -- the same code path per rank.  --gpus must equal the
+world size; more ranks than visible GPUs is refused unless OI_DIST_BACKEND=gloo
+(the one-GPU rehearsal: ranks share cuda:0, collectives on the host).
 """
 import argparse
 import json
@@ -43,7 +48,8 @@ import time
 
 import numpy as np
 
-T_PROC = time.time()
+# a rank started by launch_ranks counts its --budget-s from the launcher's start
+T_PROC = float(os.environ.get('OI_BENCH_T0', '') or time.time())
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -69,6 +75,8 @@ def parse():
                         'share --share (default: this rank\'s) -- e.g. one 8-GPU share of config 4 on one GPU')
     p.add_argument('--share', type=int, default=-1, help='day workload with --day-shares: the share to fit')
     p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--day-cells', type=int, default=0,
+                   help='day / days: only the first K cells of the day (0: all 9997) -- quick rehearsals only')
     p.add_argument('--slices', default='ordered', choices=['lpt', 'ordered'],
                    help='day slices: equal-cost LPT mixes (lpt) or consecutive runs of the '
                         'largest-n-first order (ordered)')
@@ -186,6 +194,33 @@ def pool_training_set(slices, grid_m, torch, dev):
             "r": synthetic.RADIUS_M + grid_m, "M": int(len(cat[0]))}
 
 
+def check_shares(args, world, shares):
+    """--day-shares / --share: a share run fits one share on one
+    GPU; with N ranks the day is split N ways and rank r fits share r."""
+    if args.share >= 0 and world > 1:
+        raise SystemExit("bench.py: --share picks the share of a one-GPU run; with N ranks rank r fits share r")
+    if args.share >= 0 and not args.day_shares:
+        raise SystemExit("bench.py: --share needs --day-shares")
+    if args.share >= shares:
+        raise SystemExit(f"bench.py: --share {args.share} but only {shares} shares")
+    if world > 1 and args.day_shares not in (0, world):
+        raise SystemExit(f"bench.py: --day-shares {args.day_shares} with {world} ranks would leave shares unfitted")
+
+
+def default_depth(args, world, nslices):
+    """Slices in flight beyond the one waited on, keyed on the per-rank work
+    (ADVICE r4), never on the GPU count alone:
+      * a rank's SHARE of a day (config 4 at N > 1, --day-shares runs, and the
+        season, whose every rank -- N = 1 included -- fits one 1/8 share) goes
+        into its session at once, so the rounds stay near the 1-GPU resident
+        size (8 shares at depth 20 on one GPU: 0.90 projected efficiency,
+        profiles/r04/day_share_8of8.json);
+      * a WHOLE day per rank (config 3, and `days` at any N) keeps 8 slices
+        in flight, as the headline always has."""
+    share = args.workload == 'season' or (args.workload == 'day' and (world > 1 or args.day_shares))
+    return (max(1, nslices), "every slice (a rank's share of a day)") if share else (8, "8 (a whole day per rank)")
+
+
 def build_slices(args, rank, world):
     """-> (timed slices of this rank, warmup slices, opt, config, scaling,
     cells per rank of every rank)."""
@@ -211,14 +246,15 @@ def build_slices(args, rank, world):
                 [len(parts[r]) for r in range(world)])
     if args.workload in ('day', 'days'):
         seed = args.seed + (rank if args.workload == 'days' else 0)
-        day = synthetic.make_day(seed=seed)
-        common = {"day_cells": int(day.ncell), "n_obs_per_cell": "U{300..3000}", "grid_km": 25,
+        day = synthetic.make_day(seed=seed, max_cells=args.day_cells or None)
+        common = {"day_cells": int(day.ncell), **({"day_cells_limit": args.day_cells} if args.day_cells else {}), "n_obs_per_cell": "U{300..3000}", "grid_km": 25,
                   "x0": "GPR_CS2S3.py:217", "slices": args.slices}
         day_sites = driver.site_counts(day)
         if args.workload == 'day':
             shares = max(int(args.day_shares), world)
+            check_shares(args, world, shares)
             parts = driver.lpt_partition(driver.cell_costs(day.sizes, sites=day_sites), shares)
-            idx = [args.share if (args.share >= 0 and world == 1) else r for r in range(world)]
+            idx = [args.share if args.share >= 0 else r for r in range(world)]
             mine = day.subset(parts[idx[rank]])
             mine_sites = day_sites[parts[idx[rank]]]
             if shares == world:
@@ -230,7 +266,8 @@ def build_slices(args, rank, world):
             else:
                 cfg = {"workload": (f"config 4 share: the 25km day LPT-split into {shares} GPU shares, this run "
                                     f"fits share(s) {idx} ({world} GPU), one slice per step"),
-                       **common, "cells_total": int(day.ncell), "cells_per_rank": int(mine.ncell),
+                       **common, "day_cells_total": int(day.ncell),
+                       "cells_total": int(sum(len(parts[i]) for i in idx)), "cells_per_rank": int(mine.ncell),
                        "shares": shares, "share": idx[rank],
                        "parallelism": f"{shares}-way LPT partition on E(n) m^3; {world} of them here"}
             scaling = "strong"
@@ -547,7 +584,7 @@ def main_nystrom(args, torch, dist, world, rank, gpu, cdev):
                                    + (", one blocking call per step" if args.nys_oneshot else
                                       f", one batch per step through a fit session (depth {args.depth})"),
                        "cells_per_step": ncell * world},
-            "evals_per_cell": round(float(np.mean(evals)), 2), "roofline": roofline}
+            "evals_per_cell": round(float(np.mean(evals)), 2), "roofline": roofline, **args.dist_fields}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = host_cores(args)[0]
         try:
@@ -671,7 +708,7 @@ def main_svgp(args, torch, dist, world, rank, gpu, cdev):
             "config": {"workload": f"SVGP (dev/sparseGP_example.ipynb cell 5): {k} cells x n={SVGP_N}, "
                                    f"M={SVGP_M}, B={SVGP_B}, {iters} Adam steps per rank per step",
                        "cells_per_step": k * world},
-            "failed_cells": bad, "roofline": roofline}
+            "failed_cells": bad, "roofline": roofline, **args.dist_fields}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = host_cores(args)[0]
         try:
@@ -688,6 +725,120 @@ def main_svgp(args, torch, dist, world, rank, gpu, cdev):
                 f.write(s + '\n')
     if world > 1:
         dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------- launcher
+def visible_gpus():
+    """GPUs a rank process will see, counted in a child process: the launcher
+    itself never initialises HIP (a process that has must not start the
+    ranks)."""
+    out = subprocess.run([sys.executable, '-c', 'import torch; print(torch.cuda.device_count())'],
+                         capture_output=True, text=True, timeout=600)
+    lines = out.stdout.strip().splitlines()
+    if out.returncode != 0 or not lines:
+        raise RuntimeError(f"GPU count probe failed (rc {out.returncode}): {out.stderr[-400:]}")
+    return int(lines[-1])
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(('127.0.0.1', 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None, gpus=None, backend=None, grace_s=20.0, poll_s=0.25):
+    """`bench.py --gpus N` without a launcher around it: start N rank
+    processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT in their environment, the torch.distributed.run contract),
+    forward rank 0's stdout (the JSON line) and every rank's stderr, and return
+    the exit code: 0 only if every rank exited 0 and rank 0 printed a JSON
+    line.  The first rank to fail ends the others (SIGTERM, then SIGKILL after
+    ``grace_s``) and its code is returned.  Called before this process imports
+    anything that touches the GPU; ranks are started as children, never by
+    exec.  ``gpus``: visible GPU count (probed in a child when None); N > gpus
+    is refused (exit 2) unless the backend is gloo."""
+    import signal
+    import threading
+    backend = backend or os.environ.get('OI_DIST_BACKEND', 'nccl')
+    script = script or os.path.abspath(__file__)
+    if gpus is None:
+        gpus = visible_gpus()
+    if n > gpus and backend != 'gloo':
+        log(f"--gpus {n} but only {gpus} GPU(s) visible: refusing to oversubscribe "
+            f"(OI_DIST_BACKEND=gloo rehearses N ranks on one GPU)")
+        return 2
+    port = free_port()
+    procs, lines = [], []
+
+    def pump(stream):  # rank 0's stdout -> ours, remembering the JSON lines
+        for ln in stream:
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+            if ln.lstrip().startswith('{'):
+                lines.append(ln.strip())
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+                   OI_BENCH_LAUNCHER='bench.py', OI_BENCH_T0=repr(T_PROC))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env, text=True,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    th = threading.Thread(target=pump, args=(procs[0].stdout,), daemon=True)
+    th.start()
+
+    def end_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+        t_end = time.time() + grace_s
+        for p in procs:
+            while p.poll() is None and time.time() < t_end:
+                time.sleep(0.05)
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    prev = signal.signal(signal.SIGTERM, lambda *_: (end_all(), sys.exit(143)))
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p for p in procs if p.poll() not in (None, 0)]
+            if bad:
+                rc = bad[0].returncode
+                log(f"rank {procs.index(bad[0])} exited with {rc}: ending the other ranks")
+                end_all()
+                break
+            time.sleep(poll_s)
+    finally:
+        signal.signal(signal.SIGTERM, prev)
+    th.join(timeout=5.0)
+    if rc == 0:
+        codes = [p.returncode for p in procs]
+        rc = next((c for c in codes if c != 0), 0)
+        if rc == 0 and not lines:
+            log("rank 0 printed no JSON line")
+            rc = 1
+    return rc if rc > 0 else (128 - rc if rc < 0 else 0)
+
+
+def rank_census(dist, torch, world, rank, gpu, cdev):
+    """[(rank, device index)] of every rank, by one all_gather: the line
+    reports which ranks took part and on which GPUs (``ranks_seen``)."""
+    if world == 1:
+        return [(0, gpu)]
+    mine = torch.tensor([rank, gpu], dtype=torch.int64, device=cdev)
+    allr = [torch.zeros(2, dtype=torch.int64, device=cdev) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    return sorted((int(t[0].item()), int(t[1].item())) for t in allr)
+
+
+def dist_fields(census, backend, world, args):
+    ndev = len({g for _, g in census})
+    return {"ranks_seen": [r for r, _ in census], "rank_devices": [g for _, g in census],
+            "collective_backend": (backend if world > 1 else None), "gpus_requested": args.gpus,
+            "distinct_devices": ndev,
+            "launcher": os.environ.get('OI_BENCH_LAUNCHER',
+                                       'torch.distributed.run' if 'TORCHELASTIC_RUN_ID' in os.environ
+                                       else ('external' if world > 1 else 'none'))}
 
 
 # ----------------------------------------------------------------- main
@@ -790,6 +941,9 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
 
 def main():
     args = parse()
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        # no launcher around us: start the ranks ourselves, before any GPU call
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     heartbeat()
     # one resident-cell group (one stream): OI_GROUPS=2 overlaps one group's
     # latency-bound launches with the other's GEMMs, +0.5 % on the day
@@ -805,13 +959,25 @@ def main():
     # payloads staged on the host) lets several ranks share one GPU, which is
     # how the N>1 path is rehearsed on a 1-GPU box
     backend = os.environ.get('OI_DIST_BACKEND', 'nccl')
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world}: the line would "
+                         f"misreport n_gpus")
+    ndev = torch.cuda.device_count()
+    if local >= ndev and backend != 'gloo':
+        raise SystemExit(f"bench.py: LOCAL_RANK {local} but {ndev} GPU(s) visible: refusing to put two "
+                         f"ranks on one GPU (OI_DIST_BACKEND=gloo for a one-GPU rehearsal)")
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         dist.init_process_group(backend)
-    gpu = local % max(1, torch.cuda.device_count())
+    gpu = local % max(1, ndev)
     torch.cuda.set_device(gpu)
     dev = torch.device('cuda', gpu)
     cdev = torch.device('cpu') if backend == 'gloo' else dev  # where collective tensors live
+    census = rank_census(dist, torch, world, rank, gpu, cdev)
+    args.dist_fields = dist_fields(census, backend, world, args)
+    if rank == 0:
+        log(f"world {world}: ranks {args.dist_fields['ranks_seen']} on devices "
+            f"{args.dist_fields['rank_devices']} ({backend if world > 1 else 'no collectives'})")
     if args.workload == 'nystrom':
         if args.depth is None:
             args.depth = 8
@@ -822,11 +988,7 @@ def main():
 
     slices, warm, opt, cfg, scaling, counts_all = build_slices(args, rank, world)
     if args.depth is None:
-        # a rank's share of the day (config 4: ~1250 cells in 20 slices of ~62) goes in all at once,
-        # so the session's rounds stay near the 1-GPU resident size (8 shares at depth 20 on one GPU:
-        # 0.90 projected efficiency, profiles/r04/day_share_8of8.json); a whole day on one GPU keeps
-        # 8 slices in flight
-        args.depth = 8 if (world == 1 and not args.day_shares) else max(1, len(slices))
+        args.depth, cfg["depth_rule"] = default_depth(args, world, len(slices))
     cfg["depth"] = args.depth
     x0 = X0_12P5 if args.workload == 'season' else X0
     log(f"rank {rank}: {len(slices)} slices, {sum(s.ncell for s in slices)} cells")
@@ -967,7 +1129,7 @@ def main():
             "data": "synthetic (seeded SURVEY §8d generator; reference data not shipped)",
             "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
             "failed_cells": int(np.sum(status != 0)), "timed_s": round(dt, 3),
-            "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float))}
+            "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float)), **args.dist_fields}
     if not tprof:
         line["roofline"]["timing_note"] = ("per-launch HIP-event times from a second, profiled pass over the "
                                            "same cells; the timed pass runs without per-launch events")

@@ -17,7 +17,7 @@
 //                 Householder tridiagonalisation (LAPACK dsytrd / dlatrd,
 //                 lower), three launches per column over the batch: the
 //                 column's reflector, the symmetric product over the trailing
-//                 lower triangle on SY_S workgroups per matrix, the w vector;
+//                 lower triangle on OI_SY_S workgroups per matrix, the w vector;
 //                 per 32-column panel the rank-64 trailing update on k_gemm;
 //                 V (unit lower, clean copy) and T (dlarft, forward
 //                 columnwise) kept per panel
@@ -318,16 +318,18 @@ __device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] =
 // g = p + i (panel p, i < 32) over the whole batch -- the symmetric product
 // y = A22 v streams the trailing lower triangle once per column, and one
 // workgroup per matrix could pull it only at ~40 GB/s (a CU's outstanding
-// misses bound it; measured round 4), so it is spread over SY_S workgroups
+// misses bound it; measured round 4), so it is spread over ns workgroups
 // per matrix:
 //   k_sy_reflect(p, i)  column g brought up to date with the panel's earlier
 //                       reflectors, the reflector v_g (dlarfg): d, e, tau, V
-//   k_sy_symv(p, i)     partial y of SY_S workgroups (their waves own groups of
+//   k_sy_symv(p, i)     partial y of ns workgroups (their waves own groups of
 //                       SY_C consecutive columns) and the panel dots V'v, W'v
 //   k_sy_w(p, i)        y summed in a fixed order, w = tau (y - V(W'v) - W(V'v))
 //                       - tau/2 (w'v) v, column i of the panel's T (dlarft)
 // then, per panel, the trailing update A22 -= V W' + W V' on oila::gemm.
-#define SY_S 8  // symv workgroups per matrix
+// symv workgroups per matrix: gridDim.y of k_sy_symv (OI_SY_S, default below)
+#define SY_S_DEFAULT 8
+#define SY_S_MAX TNB  // the partials live in the M x 32 H block
 __global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es, int p, int i) {
   __shared__ double red[64];
   const Eigh E = es[blockIdx.x];
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
   // reduced once at its end
   double* myw = yw + (size_t)wv * M;
   const int gw = sgrp * SY_W + wv;
-  for (int c0 = g + 1 + SY_C * gw; c0 < M; c0 += SY_C * SY_W * SY_S) {
+  const int ns = gridDim.y;
+  for (int c0 = g + 1 + SY_C * gw; c0 < M; c0 += SY_C * SY_W * ns) {
     const Rsrc rcol = rsrc(E.A + (size_t)ld * c0);
     double vc[SY_C], dot[SY_C];
 #pragma unroll
@@ -450,7 +453,7 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
         if (c0 + j < M) myw[c0 + j] += dot[j];
   }
   // panel dots, one per global wave (rows > g, 4 row chunks per load batch)
-  for (int jq = gw; jq < 2 * i; jq += SY_W * SY_S) {
+  for (int jq = gw; jq < 2 * i; jq += SY_W * ns) {
     const int q = jq % i;
     const Rsrc rc = rsrc(jq < i ? carve(E.work, M).Ws + (size_t)M * q : carve(E.work, M).Vc + (size_t)M * (p + q));
     double s4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -476,7 +479,7 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
   }
 }
 
-__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i) {
+__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i, int ns) {
   __shared__ double red[64];
   __shared__ double pan[2 * TNB];
   const Eigh E = es[blockIdx.x];
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int 
     }
     Tp[t + TNB * i] = x;
   }
-  // (4) w = tau (y - V (W'v) - W (V'v)), y = sum of the SY_S partials; then
+  // (4) w = tau (y - V (W'v) - W (V'v)), y = sum of the ns partials; then
   // w += -tau/2 (w'v) v; two rows per thread
   const gdouble* vgc = ws.Vc + (size_t)M * g;
   double sv[1] = {0.0};
@@ -512,7 +515,7 @@ __global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int 
     const bool okb = rb < M;
     double sa = 0.0, sb = 0.0;
 #pragma unroll
-    for (int s = 0; s < SY_S; ++s) {
+    for (int s = 0; s < ns; ++s) {
       sa += ws.H[(size_t)s * M + ra];
       if (okb) sb += ws.H[(size_t)s * M + rb];
     }
@@ -1131,6 +1134,11 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   const unsigned n = (unsigned)es.size();
   const size_t lds_sy = (size_t)(SY_W + 1) * Mmax * sizeof(double);
   if (lds_sy > 160 * 1024) throw LinalgErr{"eigh: matrix too large for the tridiagonalisation's LDS"};
+  static const int ns = [] {
+    const char* e = getenv("OI_SY_S");
+    const int v = e ? atoi(e) : SY_S_DEFAULT;
+    return v < 1 ? 1 : v > SY_S_MAX ? SY_S_MAX : v;
+  }();
   phase(0);
   // panel by panel: the panel's 32 reflectors on one workgroup per matrix,
   // then its trailing update A22 -= V W' + W V' (lower 64 x 64 tiles) as two
@@ -1138,8 +1146,8 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   for (int p = 0; p < std::max(Mmax - 1, 1); p += TNB) {
     for (int i = 0; i < TNB && (i == 0 || p + i < Mmax - 1); ++i) {
       hipLaunchKernelGGL(k_sy_reflect, dim3(n), dim3(SY_T), 0, st, de, p, i);
-      hipLaunchKernelGGL(k_sy_symv, dim3(n, SY_S), dim3(SY_T), lds_sy, st, de, p, i);
-      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i);
+      hipLaunchKernelGGL(k_sy_symv, dim3(n, ns), dim3(SY_T), lds_sy, st, de, p, i);
+      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i, ns);
     }
     LC(hipGetLastError());
     std::vector<Gemm> g1, g2;

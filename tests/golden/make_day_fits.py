@@ -11,7 +11,10 @@ Cells (seeded selection, written into the fixture as day indices):
     (the last bucket includes n = 3000) -- 72 cells;
   * small: 160 further cells with n < 600 (the day's smallest bucket; the
     day has no cell below n = 300) for a distributional test of the
-    evaluation count.
+    evaluation count;
+  * large (round 5, VERDICT r4 "next" item 2): 16 further cells in every
+    300-wide bucket from 600 to 3000 -- 128 cells, so that n >= 600 holds
+    192 cells and the fleet rules are decided where the cost is.
 Every cell runs in 5 observation orders: run 0 on the cell's observations as
 drawn, runs 1-4 on seeded permutations of them (the reference's chaotic
 stopping point moves with the summation order).
@@ -48,12 +51,15 @@ SELECT_SEED = 20261017
 STRATA = tuple(range(300, 3000, 300))   # bucket lower edges; width 300
 PER_STRATUM = 8
 N_SMALL = 160
+LARGE_STRATA = tuple(range(600, 3000, 300))
+LARGE_PER_STRATUM = 16
 RADIUS_KM = 325                          # >= 300 km + the lattice's half diagonal (17.7 km)
 
 
 def select_cells(sizes):
-    """-> (day indices, stratum flag): 8 per 300-wide bucket, then 160 more
-    with n < 600."""
+    """-> (day indices, stratum flag): 8 per 300-wide bucket (flag 1), then
+    160 more with n < 600 (flag 0), then 16 more per bucket from 600 to 3000
+    (flag 2; drawn from its own seed so the first 232 cells never change)."""
     import numpy as np
     rng = np.random.default_rng(SELECT_SEED)
     chosen, strat = [], []
@@ -67,6 +73,13 @@ def select_cells(sizes):
     pick = np.sort(rng.choice(pool, N_SMALL, replace=False))
     chosen += pick.tolist()
     strat += [0] * N_SMALL
+    rng2 = np.random.default_rng(SELECT_SEED + 1)
+    for lo in LARGE_STRATA:
+        hi = lo + 300 if lo < 2700 else 3001
+        pool = np.setdiff1d(np.flatnonzero((sizes >= lo) & (sizes < hi)), chosen)
+        pick = np.sort(rng2.choice(pool, LARGE_PER_STRATUM, replace=False))
+        chosen += pick.tolist()
+        strat += [2] * LARGE_PER_STRATUM
     return np.array(chosen, dtype=np.int64), np.array(strat, dtype=np.int8)
 
 

@@ -115,3 +115,29 @@ def test_two_ranks_equal_one_rank_bitwise(tmp_path):
     assert set(res) == set(ref)
     for k in ref:
         assert np.array_equal(res[k], np.asarray(ref[k]), equal_nan=True), k
+
+
+def test_bench_self_launch_gloo(tmp_path):
+    """`python bench.py --gpus 2` with no launcher around it (VERDICT r4 item
+    1): bench.py starts both ranks itself, they shard a (shortened) day over
+    one GPU with gloo collectives, and rank 0's line reports the world."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / 'line.json'
+    env = dict(os.environ, OI_DIST_BACKEND='gloo')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT'):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '4',
+                        '--warmup', '1', '--day-cells', '96', '--no-cpu-baseline', '--parity-cells', '4',
+                        '--budget-s', '90', '--out', str(out)],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line == json.loads(out.read_text())
+    assert line['n_gpus'] == 2 and line['ranks_seen'] == [0, 1] and line['rank_devices'] == [0, 0]
+    assert line['collective_backend'] == 'gloo' and line['launcher'] == 'bench.py'
+    assert line['config']['cells_total'] == 96 and line['failed_cells'] == 0
+    assert line['steps'] == 4 and not line.get('truncated')
+    assert line['parity']['pass'], line['parity']
