@@ -29,7 +29,7 @@ enum OiStatus { OI_OK = 0, OI_NOT_PD = 1 };
 // probability 50 % at sn2 / sf2 ~ 1e-18 n_obs (n = 500: 42 % at 5e-16;
 // n = 1000: 83 % at 1e-15; n = 2000: 50 % at 2e-15), 100 % below a fifth of
 // that and 0 % above 5x (tests/test_gpu_parity.py::test_duplicate_nonpd_band).
-// The m x m site form stays PD, so k_build flags the cell not-PD below the
+// The m x m site form stays PD, so k_diag_factor4w(0) flags the cell not-PD below the
 // 50 % point (and whenever sf2 + sn2 rounds to sf2).
 #define OI_DUP_NONPD_TAU 1e-18
 
@@ -88,7 +88,6 @@ extern "C" {
 #endif
 // kernel launchers (oi_kernels.hip); `cells` and `list` are device pointers,
 // `list` holds indices into `cells` sorted by T descending.
-int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT, void* stream);
 int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
 // the panels stream the L tiles and apply Dinv_jj to the finished sum (post-form)
 int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,

@@ -911,9 +911,7 @@ class Engine {
     int rc = 0;
     cur_cells = na;
     prep_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
-    mark(K_BUILD, false);
-    rc |= oi_launch_build(dc, dl_all, na, maxT, gst);
-    mark(K_BUILD, true);
+    // (no k_build since round 5: the factor kernels generate K + sn2 I where they read it)
     for (int j = 0; j < maxT; ++j) {
       int cnt = 0;
       while (cnt < na && hc(all_slots[cnt]).T > j) ++cnt;

@@ -3,7 +3,8 @@
 // for a ragged batch of independent grid cells.  Data layout: oi_device.h.
 //
 // Per objective evaluation of a cell (T = ceil(n/64) tiles per side):
-//   k_build        K + sn2 I (Matern-3/2, GPR:93-94)                         O(n^2)
+//   (K + sn2 I, Matern-3/2, GPR:93-94, is never stored: each factor kernel
+//                  generates the pristine tiles it reads from the coordinates)
 //   k_diag_factor4w(j) factor + invert diagonal tile j: one 256-thread
 //                  workgroup per cell, the tile in LDS                   ~n^2 * 64
 //   k_panel4(j) / k_panel_even(j), j even: left-looking Cholesky for the column
@@ -23,7 +24,7 @@
 //                  gradient traces sum((K^-1 - alpha alpha^T) o dK_j); K and
 //                  dK_j are regenerated from coordinates (GPR:130-138)         n^3/3
 //   k_finalize     nlZ and dnlZ (GPR:128, GPR:131-138), fixed-order sums
-// Predict (GPR:173-182): k_build (also k*), the Cholesky with the forward
+// Predict (GPR:173-182): k* = D kd* (k_diag_factor4w(0)), the Cholesky with the forward
 // substitution of r and k* folded in, then k_finalize (fs = mean + v.z,
 // sd = sqrt(sf2 - v.v), lZ from z.z): no separate triangular solves.
 //
@@ -134,83 +135,55 @@ __device__ __forceinline__ bool xcd_cell_slot_lead0(int gx, int ncell, int& cell
   return cell < ncell;
 }
 
-// ------------------------------------------------------------- k_build
-// M = D Kd D + sn2 I for tile (i, j) (K + sn2 I of GPR:93-94 / GPR:126 on the
-// sites, oi_device.h); identity on padding.
-__global__ __launch_bounds__(256) void k_build(const OiCell* __restrict__ cells,
-                                               const int32_t* __restrict__ list, int gx,
-                                               int ncell) {
-  int ci, x;
-  if (!xcd_cell_slot(gx, ncell, ci, x)) return;
-  const OiCell& c = cells[list[ci]];
-  int i, j;
-  if (!decode_tri(x, c.T, i, j)) return;
-  __shared__ double u[2][3][NB];
-  __shared__ double dws[2][NB];
-  const int t = threadIdx.x, n = c.n;
-  if (t < 2 * NB) {
-    int side = t >> 6, idx = t & 63, a = (side ? j : i) * NB + idx;
-    for (int d = 0; d < 3; ++d) u[side][d][idx] = a < n ? (SQRT3 * c.xyt[3 * a + d]) / c.hyp[d] : 0.0;
-    dws[side][idx] = a < n ? c.dw[a] : 0.0;
+// ------------------------------------------------ the covariance, generated
+// A = M = D Kd D + sn2 I for the sites (K + sn2 I of GPR:93-94 / GPR:126,
+// oi_device.h; identity on padding) is never stored (round 5: k_build, which
+// wrote it once per round only for the factor kernels to read it back, is
+// gone).  The kernel that first reads a pristine tile generates it from the
+// coordinates instead: k_diag_factor4w(0) the first diagonal tile, the even
+// panels every tile of their column j (and the partial update of column j+1),
+// k_chol_panel its column when kbeg = 0 and every look-ahead diagonal tile.
+// SiteBlk: the 64 sites of one block -- scaled coordinates sqrt(3) x_d / ell_d
+// (exactly k_build's and k_lauum_grad1's) and the site weights d, 0 past n.
+struct SiteBlk {
+  double u[3][NB];
+  double d[NB];
+};
+
+__device__ __forceinline__ void stage_sites(const OiCell& c, int b, SiteBlk* S, int t, int nt) {
+  double* dst = &S->u[0][0];
+  for (int e = t; e < 4 * NB; e += nt) {
+    const int d = e >> 6, a = b * NB + (e & 63);
+    double v = 0.0;
+    if (a < c.n) v = d < 3 ? (SQRT3 * c.xyt[3 * a + d]) / c.hyp[d] : c.dw[a];
+    dst[e] = v;
   }
-  __syncthreads();
-  const double sf2 = c.hyp[3], sn2 = c.hyp[4];
-  // Duplicate sites make K + sn2 I singular up to sn2: the reference's
-  // n x n Cholesky loses the pivot of a repeated row, (sf2 + sn2) - sf2^2 /
-  // (sf2 + sn2), to rounding (always once sf2 + sn2 rounds to sf2, sn2 = 0
-  // included; with probability 1/2 at sn2 / sf2 = OI_DUP_NONPD_TAU n_obs) and
-  // takes the LinAlgError branch (GPR:139-140); the m x m site form would not
-  // notice (oi_device.h).
-  if (x == 0 && t == 0 && c.n_obs > n && (sf2 + sn2 == sf2 || sn2 < OI_DUP_NONPD_TAU * c.n_obs * sf2))
-    *c.status = OI_NOT_PD;
-  if (i == j && t < NB) {
-    // right-hand sides of the forward substitution run inside the
-    // factorisation: z = r (site residuals), and for predict v = k* = D kd*
-    // (GPR:174, cdist of scaled coordinates)
-    const int a = i * NB + t;
-    gst(c.vec + a, a < n ? c.r[a] : 0.0);
-    if (c.mode == OI_MODE_PREDICT) {
-      double kv = 0.0;
-      if (a < n) {
-        const double xs0 = (SQRT3 * c.xs[0]) / c.hyp[0], xs1 = (SQRT3 * c.xs[1]) / c.hyp[1],
-                     xs2 = (SQRT3 * c.xs[2]) / c.hyp[2];
-        const double d0 = (SQRT3 * c.xyt[3 * a]) / c.hyp[0] - xs0;
-        const double d1 = (SQRT3 * c.xyt[3 * a + 1]) / c.hyp[1] - xs1;
-        const double d2 = (SQRT3 * c.xyt[3 * a + 2]) / c.hyp[2] - xs2;
-        const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-        kv = c.dw[a] * (sf2 * ((1.0 + Q) * exp(-Q)));
-      }
-      gst(c.vec + 3 * c.T * NB + a, kv);
-    }
+}
+
+// A[a][b] for row site a = 64 ib + r (block R) and column site b = 64 jb + q
+// (block C): (d_a d_b) sf2 (1 + Q) e^-Q (+ sn2 if a = b), Q the scaled distance
+__device__ __forceinline__ double amat(const SiteBlk& R, int r, int a, const SiteBlk& C, int q, int b, int n,
+                                       double sf2, double sn2) {
+  if (a >= n || b >= n) return a == b ? 1.0 : 0.0;
+  const double d0 = R.u[0][r] - C.u[0][q], d1 = R.u[1][r] - C.u[1][q], d2 = R.u[2][r] - C.u[2][q];
+  const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+  double v = (R.d[r] * C.d[q]) * (sf2 * ((1.0 + Q) * exp(-Q)));
+  if (a == b) v += sn2;
+  return v;
+}
+
+// a generated tile (ib, jb): element (r, q) -- row r of block ib, column q of block jb
+struct GenTile {
+  const SiteBlk* R;
+  const SiteBlk* C;
+  int ib, jb, n;
+  double sf2, sn2;
+  __device__ __forceinline__ double operator()(int r, int q) const {
+    return amat(*R, r, ib * NB + r, *C, q, jb * NB + q, n, sf2, sn2);
   }
-  double* Y = tileL(c, i, j);
-  // a diagonal tile is built on its lower triangle only (2080 entries, column-
-  // packed so whole waves retire early): the factor kernels treat the upper
-  // triangle as scratch and clear it (k_diag_factor*)
-  const int ne = i == j ? NB * (NB + 1) / 2 : OI_TILE;
-  for (int e = t; e < ne; e += 256) {
-    int r, cc;
-    if (i == j) {  // column cc starts at S(cc) = 64 cc - cc (cc - 1) / 2
-      cc = (int)((129.0 - sqrt(16641.0 - 8.0 * e)) * 0.5);
-      while (cc > 0 && NB * cc - cc * (cc - 1) / 2 > e) --cc;
-      while (NB * (cc + 1) - (cc + 1) * cc / 2 <= e) ++cc;
-      r = cc + (e - (NB * cc - cc * (cc - 1) / 2));
-    } else {
-      r = e & 63;
-      cc = e >> 6;
-    }
-    const int a = i * NB + r, b = j * NB + cc;
-    double val;
-    if (a >= n || b >= n) {
-      val = (a == b) ? 1.0 : 0.0;
-    } else {
-      double d0 = u[0][0][r] - u[1][0][cc], d1 = u[0][1][r] - u[1][1][cc], d2 = u[0][2][r] - u[1][2][cc];
-      double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-      val = (dws[0][r] * dws[1][cc]) * (sf2 * ((1.0 + Q) * exp(-Q)));  // M = D Kd D (+ sn2 I)
-      if (a == b) val += sn2;
-    }
-    gst(Y + cc * NB + r, val);
-  }
+};
+__device__ __forceinline__ GenTile gen_tile(const OiCell& c, const SiteBlk* R, int ib, const SiteBlk* C, int jb) {
+  return GenTile{R, C, ib, jb, c.n, c.hyp[3], c.hyp[4]};
 }
 
 // ------------------------------------------------- diagonal-tile helpers
@@ -250,8 +223,8 @@ __device__ long long g_diag_stamps[16];
 // ------------------------------------------ k_diag_factor4w(j)
 // Factor + invert diagonal tile j of every cell, one 256-thread workgroup per
 // cell.  The tile already holds the updated A_jj - sum_{k<j} L_jk L_jk^T
-// (the previous step's look-ahead wrote it; for j = 0 it is K + sn2 I from
-// k_build).  Writes L_jj, its log-determinant, Dinv_jj and (eval mode) W_jj.
+// (the previous step's look-ahead wrote it); for j = 0 the kernel generates
+// K + sn2 I itself and initialises the forward substitution's right-hand sides.  Writes L_jj, its log-determinant, Dinv_jj and (eval mode) W_jj.
 // Pivot <= 0 -> status = not PD (GPR:139-140); NaN pivots propagate like the
 // reference's numpy/OpenBLAS cholesky.  Four waves with the tile in LDS, for
 // latency (config 1's lone cell waits for four of these per evaluation; the
@@ -405,18 +378,70 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
   double* Y = tileL(c, j, j);
   double* zj = c.vec + j * NB;
   double* vj = c.vec + 3 * c.T * NB + j * NB;
-  // element (r, q) of the column-major tile at q*64 + r: 16 coalesced loads per
-  // thread; the upper triangle (scratch of k_build) is replaced by zeros
+  if (j == 0) {
+    // the round's first kernel for the cell.  Duplicate sites make K + sn2 I
+    // singular up to sn2: the reference's n x n Cholesky loses the pivot of a
+    // repeated row, (sf2 + sn2) - sf2^2 / (sf2 + sn2), to rounding (always once
+    // sf2 + sn2 rounds to sf2, sn2 = 0 included; with probability 1/2 at
+    // sn2 / sf2 = OI_DUP_NONPD_TAU n_obs) and takes the LinAlgError branch
+    // (GPR:139-140); the m x m site form would not notice (oi_device.h).
+    const double sf2 = c.hyp[3], sn2 = c.hyp[4];
+    if (c.n_obs > c.n && (sf2 + sn2 == sf2 || sn2 < OI_DUP_NONPD_TAU * c.n_obs * sf2)) {
+      if (t == 0) *c.status = OI_NOT_PD;
+      return;
+    }
+    // right-hand sides of the forward substitution run inside the
+    // factorisation: z = r (site residuals), and for predict v = k* = D kd*
+    // (GPR:174, cdist of scaled coordinates); block 0 also into Vs
+    const int n = c.n;
+    double xs0 = 0.0, xs1 = 0.0, xs2 = 0.0;
+    if (pred) {
+      xs0 = (SQRT3 * c.xs[0]) / c.hyp[0];
+      xs1 = (SQRT3 * c.xs[1]) / c.hyp[1];
+      xs2 = (SQRT3 * c.xs[2]) / c.hyp[2];
+    }
+    for (int a = t; a < c.T * NB; a += 256) {
+      const double z = a < n ? c.r[a] : 0.0;
+      gst(c.vec + a, z);
+      double kv = 0.0;
+      if (pred && a < n) {
+        const double d0 = (SQRT3 * c.xyt[3 * a]) / c.hyp[0] - xs0;
+        const double d1 = (SQRT3 * c.xyt[3 * a + 1]) / c.hyp[1] - xs1;
+        const double d2 = (SQRT3 * c.xyt[3 * a + 2]) / c.hyp[2] - xs2;
+        const double Q = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        kv = c.dw[a] * (sf2 * ((1.0 + Q) * exp(-Q)));
+      }
+      if (pred) gst(c.vec + 3 * c.T * NB + a, kv);
+      if (a < NB) {
+        Vs[a] = z;
+        Vs[NB + a] = kv;
+      }
+    }
+    // tile (0, 0) generated from the sites (lower triangle; zeros above)
+    SiteBlk* sb = (SiteBlk*)Xs;
+    stage_sites(c, 0, sb, t, 256);
+    lds_barrier();
+    const GenTile A0 = gen_tile(c, sb, 0, sb, 0);
+#pragma unroll 4
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      As[r * DW_LD + q] = r >= q ? A0(r, q) : 0.0;
+      Is[r * DW_LD + q] = 0.0;
+    }
+  } else {
+    // element (r, q) of the column-major tile at q*64 + r: 16 coalesced loads per
+      // thread; the upper triangle (scratch of the look-ahead) is replaced by zeros
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int e = t + 256 * u, q = e >> 6, r = e & 63;
-    const double v = gld(Y + e);
-    As[r * DW_LD + q] = r >= q ? v : 0.0;
-    Is[r * DW_LD + q] = 0.0;
-  }
-  if (t < NB) {
-    Vs[t] = zj[t];
-    Vs[NB + t] = pred ? vj[t] : 0.0;
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      const double v = gld(Y + e);
+      As[r * DW_LD + q] = r >= q ? v : 0.0;
+      Is[r * DW_LD + q] = 0.0;
+    }
+    if (t < NB) {
+      Vs[t] = zj[t];
+      Vs[NB + t] = pred ? vj[t] : 0.0;
+    }
   }
   lds_barrier();
   DIAG_STAMP(1);
@@ -607,7 +632,7 @@ __device__ __forceinline__ void alpha_update(const OiCell& c, const double* X, i
 //   L_ij^T  = Dinv_jj (A_ij^T - sum_{k=kbeg}^{j-1} L_jk L_ik^T)
 //   W_j,jj  = Dinv_jj (Vneg - sum_{k=kfirst}^{j-1} L_jk W_k,jj)   (Vneg = 0 if kfirst = jj)
 // out(m, n) = sum_q Dinv[m][q] S(q, n), S(m, n) = base[m*64 + n] - acc(m, n)
-// (base null: S = -acc).  S is staged in LDS at row stride LDSA = 80 (B operand:
+// (base null: the generated pristine tile, gen(n, m); both null: S = -acc).  S is staged in LDS at row stride LDSA = 80 (B operand:
 // rows k, k+1 of a 32-lane ds_read_b64 in opposite bank halves); Dinv_jj (column-major,
 // lower triangular, zero above the diagonal) is read into registers once, all
 // loads in flight together.  The 160 block-k-steps of the triangular product
@@ -615,8 +640,8 @@ __device__ __forceinline__ void alpha_update(const OiCell& c, const double* X, i
 // blocks 2(w>>1), 2(w>>1)+1 -- 40 MFMAs per wave.  The result is written to
 // dst[m*64 + n] and staged in lds as X[m*XLD + n] (what fwd_update /
 // alpha_update and the look-ahead read).
-__device__ __forceinline__ void post_left(const Quad& acc, double* lds, const double* base, const double* Dj,
-                                          double* dst) {
+__device__ __forceinline__ void post_left(const Quad& acc, double* lds, const double* base, const GenTile* gen,
+                                          const double* Dj, double* dst) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int mA = (w & 1) ? 1 : 0, mB = 3 - mA, n0 = 2 * (w >> 1);
@@ -627,7 +652,9 @@ __device__ __forceinline__ void post_left(const Quad& acc, double* lds, const do
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        bv[(2 * mb + nb) * 4 + r] = base ? gld(base + acc1_row(mb, r) * NB + acc1_col(nb)) : 0.0;
+        bv[(2 * mb + nb) * 4 + r] = base  ? gld(base + acc1_row(mb, r) * NB + acc1_col(nb))
+                                    : gen ? (*gen)(acc1_col(nb), acc1_row(mb, r))
+                                          : 0.0;
   __syncthreads();  // the GEMM's last LDS reads are done
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb)
@@ -676,6 +703,10 @@ __device__ __forceinline__ void post_left(const Quad& acc, double* lds, const do
   __syncthreads();
 }
 
+// GEN = (kbeg == 0): the column's A_ij are still pristine and generated here
+// (its own instantiation: the generating epilogue would cost the common
+// kbeg = j - 1 launches a wave per SIMD)
+template <bool GEN>
 __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ cells,
                                                    const int32_t* __restrict__ list, int j,
                                                    int kbeg, int gx, int ncell) {
@@ -702,7 +733,18 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       a = tileL(c, j, kbeg + p);
       b = tileL(c, i, kbeg + p);
     });
-    post_left(acc, lds, Y, Dj, Y);  // L_ij^T = Dinv_jj (A_ij^T - acc), stored and staged
+    // kbeg = 0 (j = 1 of the paired scheme, every j of OI_PANEL=1): A_ij is still
+    // pristine -- generated from the sites (the GEMM's last barrier freed lds)
+    if (GEN) {
+      SiteBlk* sbl = (SiteBlk*)lds;
+      stage_sites(c, i, &sbl[0], threadIdx.x, 256);
+      stage_sites(c, j, &sbl[1], threadIdx.x, 256);
+      __syncthreads();
+      const GenTile Aij = gen_tile(c, &sbl[0], i, &sbl[1], j);
+      post_left(acc, lds, nullptr, &Aij, Dj, Y);  // L_ij^T = Dinv_jj (A_ij^T - acc), stored and staged
+    } else {
+      post_left(acc, lds, Y, nullptr, Dj, Y);
+    }
     fwd_update<256>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) return;
     // ---- look-ahead: diagonal tile j+1 = i.
@@ -733,12 +775,17 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       a = tileL(c, i, p);
       b = a;
     });
+    // the diagonal tile is pristine here (no earlier step touches it): generated
     double* Yd = tileL(c, i, i);
+    SiteBlk* sbd = (SiteBlk*)lds;
+    stage_sites(c, i, sbd, threadIdx.x, 256);
+    __syncthreads();
+    const GenTile Ad = gen_tile(c, sbd, i, sbd, i);
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
         for (int r = 0; r < 4; ++r) {
           const int m = acc1_row(mb, r), n = acc1_col(nb);
-          gst(Yd + m * NB + n, gld(Yd + m * NB + n) - accd.c[mb][nb][r]);
+          gst(Yd + m * NB + n, Ad(n, m) - accd.c[mb][nb][r]);
         }
     return;
   }
@@ -757,7 +804,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
     a = tileL(c, j, kfirst + p);
     b = tileW(c, kfirst + p, jj);
   }, cm);
-  post_left(acc, lds, extra ? Wt : nullptr, Dj, Wt);  // W_j,jj = Dinv_jj (Vneg - acc), stored and staged
+  post_left(acc, lds, extra ? Wt : nullptr, nullptr, Dj, Wt);  // W_j,jj = Dinv_jj (Vneg - acc), stored and staged
   alpha_update<256>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
 }
 
@@ -778,11 +825,28 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
 //                              by k_chol_panel(j+1, kbeg=j))
 // Accumulators come out transposed with respect to the tile storage, so each
 // 64x64 half goes through LDS and is written back with coalesced 16 B rows.
-enum { EMIT_STORE = 0, EMIT_SUB = 1, EMIT_NEG = 2 };
+enum { EMIT_STORE = 0, EMIT_SUB = 1, EMIT_NEG = 2, EMIT_GENSUB = 3 };
 
-// dst[n*64 + m] (op)= D_h[m][n] for the 64x64 half h of a gemm2 accumulator.
+// dst[n*64 + m] (op)= X[n*XLD + m] for a tile staged in lds
+__device__ __forceinline__ void emit_copy(const double* X, double* dst, int op, const GenTile* gen = nullptr) {
+  for (int e = threadIdx.x; e < OI_TILE; e += GEMM_THREADS) {
+    const double v = X[(e >> 6) * XLD + (e & 63)];
+    if (op == EMIT_STORE)
+      gst(dst + e, v);
+    else if (op == EMIT_SUB)
+      gst(dst + e, gld(dst + e) - v);
+    else if (op == EMIT_GENSUB)
+      gst(dst + e, (*gen)(e & 63, e >> 6) - v);
+    else
+      gst(dst + e, -v);
+  }
+}
+
+// dst[n*64 + m] (op)= D_h[m][n] for the 64x64 half h of a gemm2 accumulator
+// (EMIT_GENSUB: dst = A - D_h, A the pristine tile generated by *gen).
 // Leaves the staged tile in X[n*XLD + m] (= dst's storage order) for reuse.
-__device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, double* dst, int op) {
+__device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, double* dst, int op,
+                                          const GenTile* gen = nullptr) {
   const int w = threadIdx.x >> 6;
   __syncthreads();
   if (((w & 3) >> 1) == h) {
@@ -792,35 +856,14 @@ __device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, dou
           X[(acc_col(nb) - 64 * h) * XLD + acc_row(mb, r)] = acc.c[mb][nb][r];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < OI_TILE; e += GEMM_THREADS) {
-    const double v = X[(e >> 6) * XLD + (e & 63)];
-    if (op == EMIT_STORE)
-      gst(dst + e, v);
-    else if (op == EMIT_SUB)
-      gst(dst + e, gld(dst + e) - v);
-    else
-      gst(dst + e, -v);
-  }
-}
-
-// dst[n*64 + m] (op)= X[n*XLD + m] for a tile staged in lds (second half of emit_half)
-__device__ __forceinline__ void emit_copy(const double* X, double* dst, int op) {
-  for (int e = threadIdx.x; e < OI_TILE; e += GEMM_THREADS) {
-    const double v = X[(e >> 6) * XLD + (e & 63)];
-    if (op == EMIT_STORE)
-      gst(dst + e, v);
-    else if (op == EMIT_SUB)
-      gst(dst + e, gld(dst + e) - v);
-    else
-      gst(dst + e, -v);
-  }
+  emit_copy(X, dst, op, gen);
 }
 
 // Post-form (POST): half 0 accumulates sum_{k<j} L_ik L_jk^T (factor) or
 // sum_k W_k,jj^T L_jk^T (W rows) and is finished by post_right:
 //   L_ij = (A_ij - acc) Dinv_jj^T,   W_j,jj^T = -acc Dinv_jj^T.
-// out(m, n) = sum_q S(m, q) Dinv[n][q], S(m, n) = base[n*64 + m] - acc(m, n)
-// (base null: S = -acc).  S is staged in LDS row-major at S[m*SLD + q] (A
+// out(m, n) = sum_q S(m, q) Dinv[n][q], S(m, n) = A(m, n) - acc(m, n), A the
+// pristine tile generated from the sites (base null: S = -acc).  S is staged in LDS row-major at S[m*SLD + q] (A
 // operand, SLD = 66: the ds_read_b64 of rows k, k+1 by one 32-lane group land
 // on disjoint banks, 4m + 2k mod 64, and the accumulator write-back is 16
 // consecutive doubles per lane group) and Dinv_jj's ten lower 16x16 blocks
@@ -835,7 +878,7 @@ __device__ __forceinline__ void emit_copy(const double* X, double* dst, int op) 
 #define SLD 66
 #define DPK_OFF (NB * SLD)
 static_assert(DPK_OFF + 10 * 256 <= GEMM2_LDS, "post_right staging must fit the GEMM LDS");
-__device__ __forceinline__ void post_right(const Quad& acc, double* lds, const double* base, const double* Dj) {
+__device__ __forceinline__ void post_right(const Quad& acc, double* lds, const GenTile* base, const double* Dj) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const bool mine = (w & 3) < 2;  // the waves holding half 0
@@ -853,7 +896,7 @@ __device__ __forceinline__ void post_right(const Quad& acc, double* lds, const d
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        bv[(2 * mb + nb) * 4 + r] = (mine && base) ? gld(base + acc_col(nb) * NB + acc_row(mb, r)) : 0.0;
+        bv[(2 * mb + nb) * 4 + r] = (mine && base) ? (*base)(acc_row(mb, r), acc_col(nb)) : 0.0;
   __syncthreads();  // the GEMM's last LDS reads are done
   if (mine) {
 #pragma unroll
@@ -895,6 +938,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
                                                             const int32_t* __restrict__ list,
                                                             int j, int gx, int ncell) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
+  __shared__ SiteBlk sb[3];  // sites of block row i, block columns j, j+1
   static_assert(NB * XLD <= GEMM2_LDS, "staging tile must fit the GEMM LDS");
   int ci, x;
   if (!xcd_cell_slot(gx, ncell, ci, x)) return;
@@ -919,16 +963,22 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
     // blocks above the diagonal are never read
     const unsigned sk = pad_skip(32 * wr, 32 * (wc & 1), mlim, nlim) |
                         (x == 0 && wc >= 2 ? upper_blocks(32 * wr, 32 * (wc - 2)) : 0u);
+    stage_sites(c, i, &sb[0], threadIdx.x, GEMM_THREADS);  // read after the GEMM's barriers
+    stage_sites(c, j, &sb[1], threadIdx.x, GEMM_THREADS);
+    stage_sites(c, j + 1, &sb[2], threadIdx.x, GEMM_THREADS);
     gemm2_kmajor<true>(acc, lds, j, [=, &c](int p, const double*& a, const double*& b0, const double*& b1) {
       a = tileL(c, i, p);
       b0 = tileL(c, j, p);
       b1 = tileL(c, j + 1, p);
     }, sk);
-    post_right(acc, lds, tileL(c, i, j), Dj);  // L_ij = (A_ij - acc) Dinv_jj^T, staged
+    if (j == 0) __syncthreads();  // no GEMM ran: the staged sites need a barrier
+    const GenTile Aij = gen_tile(c, &sb[0], i, &sb[1], j), Ai1 = gen_tile(c, &sb[0], i, &sb[2], j + 1);
+    post_right(acc, lds, &Aij, Dj);  // L_ij = (A_ij - acc) Dinv_jj^T, staged
     emit_copy(lds, tileL(c, i, j), EMIT_STORE);
     fwd_update<GEMM_THREADS>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) {
-      if (j > 0) emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_SUB);  // partial update of A_i,j+1 (empty at j = 0)
+      // partial update of A_i,j+1 (empty at j = 0: k_chol_panel(1, kbeg = 0) generates the tile)
+      if (j > 0) emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_GENSUB, &Ai1);
       return;
     }
     // i = j+1: add the fresh L_j+1,j L_j+1,j^T (staged in lds as X[q*XLD + m] =
@@ -951,7 +1001,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
         }
       }
     }
-    emit_half(acc, 1, lds, tileL(c, i, i), EMIT_SUB);
+    emit_half(acc, 1, lds, tileL(c, i, i), EMIT_GENSUB, &Ai1);  // i = j+1: A_j+1,j+1 - acc
     return;
   }
   const int jj = x - ntrsm;
@@ -1015,7 +1065,7 @@ __device__ __forceinline__ void stage4_q1(const Quad8& acc, int qr, double* X) {
 // wave w computes row block w & 3 of both tiles against column blocks {0, 3}
 // (w < 4) or {1, 2} (20 + 20 MFMAs); returns with the products in o[r][0..1].
 __device__ __forceinline__ void post_right4x2(const Quad8& acc, double* lds, const double* Dj, bool two,
-                                              const double* A0, const double* A1, d4 (&o)[2][2]) {
+                                              const GenTile* A0, const GenTile* A1, d4 (&o)[2][2]) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int mb = w & 3, nA = (w >> 2) ? 1 : 0, nB = 3 - nA;
@@ -1038,10 +1088,10 @@ __device__ __forceinline__ void post_right4x2(const Quad8& acc, double* lds, con
   for (int kk = 0; kk < 8; ++kk) bA[kk] = kk <= 4 * nA + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * nA + fr) : 0.0;
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) bB[kk] = kk <= 4 * nB + 3 ? gld(Dj + (4 * kk + fk) * NB + 16 * nB + fr) : 0.0;
-  if (A0) {  // S_r += A_r: element (m, q) at q*64 + m, 8 per thread and tile.  A wave-
-    // instruction covers 32 rows m x 2 columns q (lane l: m = m0 + l/2, q = q0 + l%2):
-    // the global reads are two 256-B runs, and S[m*SLD + q] (bank 4m + 2q) hits 64
-    // distinct banks per 32-lane read and 32 per 16-lane write (2m + q distinct mod 16)
+  if (A0) {  // S_r += A_r, A_r generated: element (m, q), 8 per thread and tile.  A
+    // wave-instruction covers 32 rows m x 2 columns q (lane l: m = m0 + l/2, q = q0 + l%2):
+    // S[m*SLD + q] (bank 4m + 2q) hits 64 distinct banks per 32-lane read and 32 per
+    // 16-lane write (2m + q distinct mod 16)
     double av[8], bv[8];
     int ix[8];
 #pragma unroll
@@ -1049,8 +1099,8 @@ __device__ __forceinline__ void post_right4x2(const Quad8& acc, double* lds, con
       const int g = t + GEMM_THREADS * u, b = g >> 6, l = g & 63;
       const int m = 32 * (b & 1) + (l >> 1), q = 2 * (b >> 1) + (l & 1);
       ix[u] = m * SLD + q;
-      av[u] = gld(A0 + q * NB + m);
-      bv[u] = two ? gld(A1 + q * NB + m) : 0.0;
+      av[u] = (*A0)(m, q);
+      bv[u] = two ? (*A1)(m, q) : 0.0;
     }
     __syncthreads();
 #pragma unroll
@@ -1090,6 +1140,7 @@ __device__ __forceinline__ void stage_post4(const d4 (&o)[2][2], int r, double* 
 __global__ __launch_bounds__(GEMM_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list, int j, int gx, int ncell) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM4_LDS];
+  __shared__ SiteBlk sb[4];  // sites of block rows i1, i2 and block columns j, j+1 (80 KiB in all: 2 per CU)
   static_assert(2 * NB * SLD <= GEMM4_LDS && 2 * NB * XLD <= GEMM4_LDS, "panel4 staging must fit");
   int ci, x;
   if (!xcd_cell_slot(gx, ncell, ci, x)) return;
@@ -1125,11 +1176,17 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
       b1 = tileL(c, j + 1, p);
     };
     const bool masked = x == 0 || i2 >= T - 1 || j + 1 == T - 1;
+    stage_sites(c, i1, &sb[0], t, GEMM_THREADS);  // read after the GEMM's barriers
+    stage_sites(c, i2, &sb[1], t, GEMM_THREADS);
+    stage_sites(c, j, &sb[2], t, GEMM_THREADS);
+    stage_sites(c, j + 1, &sb[3], t, GEMM_THREADS);
     if (masked)
       gemm4_kmajor<true>(acc, lds, 4 * j, skip, fpair);
     else
       gemm4_kmajor<false>(acc, lds, 4 * j, 0u, fpair);
-    __syncthreads();  // the GEMM's last LDS reads are done
+    __syncthreads();  // the GEMM's last LDS reads are done (and the sites are staged)
+    const GenTile A1j = gen_tile(c, &sb[0], i1, &sb[2], j), A2j = gen_tile(c, &sb[1], i2, &sb[2], j);
+    const GenTile A1n = gen_tile(c, &sb[0], i1, &sb[3], j + 1), A2n = gen_tile(c, &sb[1], i2, &sb[3], j + 1);
     // column j+1: partial updates of A_{i_r, j+1} (x = 0: the diagonal tile, whose
     // L_{j+1,j} L_{j+1,j}^T part follows once that tile is final); at j = 0 the
     // sums are empty and A - 0 is A bit for bit: no round trip through HBM
@@ -1137,11 +1194,11 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
       stage4_q1(acc, 0, lds);
       if (two) stage4_q1(acc, 1, lds + NB * XLD);
       __syncthreads();
-      emit_copy(lds, tileL(c, i1, j + 1), EMIT_SUB);
-      if (two) emit_copy(lds + NB * XLD, tileL(c, i2, j + 1), EMIT_SUB);
+      emit_copy(lds, tileL(c, i1, j + 1), EMIT_GENSUB, &A1n);
+      if (two) emit_copy(lds + NB * XLD, tileL(c, i2, j + 1), EMIT_GENSUB, &A2n);
       __syncthreads();
     }
-    post_right4x2(acc, lds, Dj, two, tileL(c, i1, j), two ? tileL(c, i2, j) : nullptr, o);
+    post_right4x2(acc, lds, Dj, two, &A1j, two ? &A2j : nullptr, o);
     const double pre1 = fwd_preload(c, i1, j);
     const double pre2 = two ? fwd_preload(c, i2, j) : 0.0;
     __syncthreads();
@@ -1169,7 +1226,11 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
         for (int r = 0; r < 4; ++r) Y[(16 * bn + fr) * XLD + 16 * bm + (lane >> 4) + 4 * r] = s[r];
       }
       __syncthreads();
-      emit_copy(Y, tileL(c, i1, i1), EMIT_SUB);
+      // j > 0: the tile holds A - (sum over k < j) from above; j = 0: still pristine
+      if (j > 0)
+        emit_copy(Y, tileL(c, i1, i1), EMIT_SUB);
+      else
+        emit_copy(Y, tileL(c, i1, i1), EMIT_GENSUB, &A1n);
     }
     if (!two) return;
     __syncthreads();
@@ -1553,15 +1614,6 @@ static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 static inline int ret() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 static inline unsigned grid1(int gx, int ncell) { return (unsigned)gx * (unsigned)((ncell + 7) & ~7); }
 
-extern "C" int oi_launch_build(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                               void* stream) {
-  if (ncell <= 0 || maxT <= 0) return 0;
-  const int gx = maxT * (maxT + 1) / 2;
-  hipLaunchKernelGGL(k_build, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, gx,
-                     ncell);
-  return ret();
-}
-
 extern "C" int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j,
                                      void* stream) {
   if (ncell <= 0) return 0;
@@ -1573,8 +1625,12 @@ extern "C" int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, in
                                     int j, int kbeg, int with_trtri, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
-  hipLaunchKernelGGL(k_chol_panel, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, kbeg, gx,
-                     ncell);
+  if (kbeg == 0)
+    hipLaunchKernelGGL(k_chol_panel<true>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, kbeg,
+                       gx, ncell);
+  else
+    hipLaunchKernelGGL(k_chol_panel<false>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, kbeg,
+                       gx, ncell);
   return ret();
 }
 
