@@ -70,6 +70,9 @@ def parse():
     p.add_argument('--season-shares', type=int, default=8,
                    help='season workload: the 12.5 km day is LPT-split into this many GPU shares; rank r '
                         'fits share r (config 5 = 8 shares on 8 GPUs; at N = 1 one 1/8 share)')
+    p.add_argument('--season-days', type=int, default=1,
+                   help='season workload: consecutive season days (seed + d) whose share r rank r fits, in order, '
+                        'through one session (config 5 is 30 days on 8 GPUs)')
     p.add_argument('--day-shares', type=int, default=0,
                    help='day workload: LPT-split the day into this many GPU shares (default: one per rank) and fit '
                         'share --share (default: this rank\'s) -- e.g. one 8-GPU share of config 4 on one GPU')
@@ -228,22 +231,35 @@ def build_slices(args, rank, world):
     warm = [synthetic.make_cells(np.random.default_rng(900 + g).integers(300, 1201, 24),
                                  seed=1000 + 97 * g + rank) for g in range(args.warmup)]
     if args.workload == 'season':
+        # config 5: rank r fits share r of each of --season-days consecutive
+        # season days (seed + d), the days one after another through one
+        # session; each day's share in ~steps/K slices of equal estimated cost
         shares = max(int(args.season_shares), world)
-        cen, sizes = synthetic.season_day_plan(seed=args.seed)
-        est = driver.expected_sites(sizes, grid_m=synthetic.GRID_12P5_M)
-        parts = driver.lpt_partition(driver.cell_costs(sizes, sites=est), shares)
-        mine = synthetic.season_cells(cen, sizes, parts[rank], seed=args.seed)
-        cfg = {"workload": (f"config 5: one day of the 12.5 km season (640x640 grid, {len(sizes)} cells, "
-                            f"n ~ U{{300..5000}}), opt=True fit+predict; LPT-split into {shares} GPU shares, "
-                            f"this run fits {world} of them (share r on rank r), one slice per step"),
-               "day_cells": int(len(sizes)), "n_obs_per_cell": "U{300..5000}", "grid_km": 12.5,
-               "x0": "GPR_CS2S3.py:217 with grid_res = 12.5", "shares": shares,
-               "cells_total": int(sum(len(parts[r]) for r in range(world))), "cells_per_rank": int(mine.ncell),
+        K = max(1, int(args.season_days))
+        per_day = [args.steps // K + (1 if d < args.steps % K else 0) for d in range(K)]
+        out, ncell_day, tot, mine_n, counts = [], 0, 0, 0, [0] * world
+        for d in range(K):
+            cen, sizes = synthetic.season_day_plan(seed=args.seed + d)
+            est = driver.expected_sites(sizes, grid_m=synthetic.GRID_12P5_M)
+            parts = driver.lpt_partition(driver.cell_costs(sizes, sites=est), shares)
+            mine = synthetic.season_cells(cen, sizes, parts[rank], seed=args.seed + d)
+            sl = split_slices(mine.sizes, max(1, per_day[d]), args.slices, driver.site_counts(mine))
+            out += [mine.subset(s) for s in sl]
+            ncell_day = len(sizes)
+            tot += int(sum(len(parts[r]) for r in range(world)))
+            mine_n += int(mine.ncell)
+            for r in range(world):
+                counts[r] += len(parts[r])
+        days = "one day" if K == 1 else f"{K} consecutive days (seeds {args.seed}..{args.seed + K - 1})"
+        cfg = {"workload": (f"config 5: {days} of the 12.5 km season (640x640 grid, {ncell_day} cells a day, "
+                            f"n ~ U{{300..5000}}), opt=True fit+predict; each day LPT-split into {shares} GPU "
+                            f"shares, this run fits {world} of them (share r on rank r), the days in order through "
+                            f"one session, one slice per step"),
+               "day_cells": int(ncell_day), "season_days": K, "n_obs_per_cell": "U{300..5000}", "grid_km": 12.5,
+               "x0": "GPR_CS2S3.py:217 with grid_res = 12.5", "shares": shares, "slices_per_day": per_day,
+               "cells_total": tot, "cells_per_rank": mine_n,
                "parallelism": f"dp{world} ({shares}-way LPT partition on E(n) m^3, m = expected sites)"}
-        sites = driver.site_counts(mine)
-        sl = split_slices(mine.sizes, args.steps, args.slices, sites)
-        return ([mine.subset(s) for s in sl], warm, True, cfg, "weak",
-                [len(parts[r]) for r in range(world)])
+        return out, warm, True, cfg, "weak", counts
     if args.workload in ('day', 'days'):
         seed = args.seed + (rank if args.workload == 'days' else 0)
         day = synthetic.make_day(seed=seed, max_cells=args.day_cells or None)
@@ -970,6 +986,9 @@ def main():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         dist.init_process_group(backend)
     gpu = local % max(1, ndev)
+    per_dev = -(-world // max(1, ndev))  # ranks sharing one GPU (the gloo rehearsal)
+    if per_dev > 1:  # each rank's library arena takes a share of the HBM, not 60 % of what is left
+        os.environ.setdefault('OI_ARENA_FRAC', f"{0.8 / per_dev:.4f}")
     torch.cuda.set_device(gpu)
     dev = torch.device('cuda', gpu)
     cdev = torch.device('cpu') if backend == 'gloo' else dev  # where collective tensors live
@@ -1120,7 +1139,7 @@ def main():
     evals = info[:, 3].astype(float) if opt else np.zeros(len(sizes_timed))
     n = sites_timed.astype(float)
     metric = (METRIC if args.workload in ('day', 'days') else
-              "grid-cells/sec (full GP fit+predict), 12.5 km season day, fp64" if args.workload == 'season' else
+              "grid-cells/sec (full GP fit+predict), 12.5 km season, fp64" if args.workload == 'season' else
               f"grid-cells/sec ({args.workload}), fp64")
     line = {"metric": metric,
             "value": round(total_cells / dt, 4), "unit": "grid-cells/s", "n_gpus": world,

@@ -406,7 +406,14 @@ Context& context(int device, int64_t pool_bytes) {
     if (p->arena_bytes == SIZE_MAX - 1) return *p;  // keep the automatic arena between calls
     size_t fr = 0, tot = 0;
     HIPC(hipMemGetInfo(&fr, &tot));
-    want = (size_t)(fr * 0.6);
+    // OI_ARENA_FRAC: the share of free HBM the automatic arena takes (0.6);
+    // bench.py lowers it when several rank processes share one GPU
+    static const double frac = [] {
+      const char* e = getenv("OI_ARENA_FRAC");
+      const double f = e ? atof(e) : 0.6;
+      return f > 0.0 && f <= 0.95 ? f : 0.6;
+    }();
+    want = (size_t)(fr * frac);
   }
   if (want != p->arena_bytes && p->live_sessions == 0) {
     p->arena.~Arena();
@@ -917,9 +924,13 @@ class Engine {
       while (cnt < na && hc(all_slots[cnt]).T > j) ++cnt;
       cur_j = j;
       cur_cells = cnt;
-      mark(K_CHOL, false);
-      rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, gst);
-      mark(K_CHOL, true);
+      // diagonal tile 0 has its own launch; tile j+1 is factored by the
+      // look-ahead workgroup of column j's panel launch (round 5)
+      if (j == 0) {
+        mark(K_CHOL, false);
+        rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, gst);
+        mark(K_CHOL, true);
+      }
       const bool even = !legacy_ && (j % 2 == 0);
       const int kbeg = (legacy_ || even) ? 0 : j - 1;
       // the last column of a round with no fitting cell has neither factor
@@ -958,9 +969,11 @@ class Engine {
     cur_cells = ne;
     // z = L^-1 r and alpha = W^T z were built during the factorisation
     // (k_diag_factor and the panels), quad = z^T z
-    mark(K_LAUUM, false);
-    rc |= oi_launch_lauum_grad(dc, dl_ev, ne, maxTe, gst);
-    mark(K_LAUUM, true);
+    if (ne > 0) {  // (an empty launch would still be profiled)
+      mark(K_LAUUM, false);
+      rc |= oi_launch_lauum_grad(dc, dl_ev, ne, maxTe, gst);
+      mark(K_LAUUM, true);
+    }
     // nlZ / dnlZ of the fitting cells and fs / sd / lZ of the predicting ones
     cur_cells = na;
     // the host spins on the group's flag (profiling rounds synchronise the

@@ -289,7 +289,7 @@ __device__ __forceinline__ double potrf4w(double* As) {
     // 6 / 3 / 1 blocks of 16 x 16 over the four waves; the diagonal blocks'
     // upper halves are scratch until their panel writes zeros back
     const int nblk = (3 - J) * (4 - J) / 2;
-    for (int b = w; b < nblk; b += 4) {
+    for (int b = w; w < 4 && b < nblk; b += 4) {
       int I = J + 1, rem = b;
       while (rem >= I - J) {
         rem -= I - J;
@@ -306,11 +306,24 @@ __device__ __forceinline__ double potrf4w(double* As) {
   return dmin;
 }
 
-// Is <- L^-1 of the factored tile in As (row-major, stride DW_LD); Is must
-// hold zeros in its blocks above the diagonal.  Xs: 4 x 16 x 17 scratch.
-__device__ __forceinline__ void trtri4w(const double* As, double* Is, double* Xs) {
+// Packed storage (round 5): the factored tile keeps L in the lower triangle of
+// As (row-major, stride DW_LD = 65) and its inverse in the strict upper one --
+// Inv[R][C] (R >= C) at As[C * DW_LD + R + 1] -- so the diagonal factor needs
+// one 64 x 65 array (33 KB) and fits in a panel kernel's LDS (the look-ahead
+// workgroup of every panel launch factors the next diagonal tile itself).
+__device__ __forceinline__ double& inv_at(double* As, int R, int C) { return As[C * DW_LD + R + 1]; }
+__device__ __forceinline__ double inv_get(const double* As, int R, int C) {
+  return R >= C ? As[C * DW_LD + R + 1] : 0.0;
+}
+
+// Inv <- L^-1 of the factored tile in As (packed, above); waves 0..3 work, every
+// wave of the workgroup takes the barriers (so 512-thread callers may run it).
+// dump: 64 doubles of scratch (the zeros above the diagonal of each column's
+// x are stored there rather than under a per-element branch: a conditional
+// store with a lane-dependent bound made the compiler take 256 VGPRs)
+__device__ __forceinline__ void trtri4w(double* As, double* dump) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = lane >> 4;
-  {
+  if (w < 4) {
     // column fr of Inv_ww: x = L_ww^-1 e_fr, right-looking (x_i final once the
     // columns before it are applied; the updates of later rows are independent),
     // x_i scaled by 1/L_ii as LAPACK's dtrti2 does (lane i holds 1/L_ii)
@@ -327,53 +340,49 @@ __device__ __forceinline__ void trtri4w(const double* As, double* Is, double* Xs
     }
     if (fk == 0)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) Is[(o + i) * DW_LD + o + fr] = x[i];
+      for (int i = 0; i < 16; ++i) *(i >= fr ? &inv_at(As, o + i, o + fr) : dump + lane) = x[i];
   }
   lds_barrier();
   DIAG_STAMP(4);
-  // ---------------- off-diagonal blocks by levels (wave w: J = w, I = J + lev)
-  double* Xw = Xs + w * 272;
+  // ---------------- off-diagonal blocks by levels (wave w: J = w, I = J + lev):
+  // X = sum_K L_IK Inv_KJ on the MFMA unit, then Inv_IJ = -Inv_II X with X
+  // taken straight from the accumulator (lane (fk, fr) holds X[fk + 4q][fr],
+  // exactly the B operand of k-step q)
 #pragma unroll
   for (int lev = 1; lev < 4; ++lev) {
     const int Jb = w, Ib = w + lev;
-    const bool act = Ib < 4;
-    if (act) {
+    if (w < 4 && Ib < 4) {
       d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
       for (int K = Jb; K < Ib; ++K)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int k = 4 * kk + fk;
-          acc = MFMA64(As[(16 * Ib + fr) * DW_LD + 16 * K + k], Is[(16 * K + k) * DW_LD + 16 * Jb + fr], acc);
+          acc = MFMA64(As[(16 * Ib + fr) * DW_LD + 16 * K + k], inv_get(As, 16 * K + k, 16 * Jb + fr), acc);
         }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Xw[(fk + 4 * q) * 17 + fr] = acc[q];  // Xw[k][n] = X[k][n]
-    }
-    lds_barrier();
-    if (act) {
       d4 y = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int k = 4 * kk + fk;
-        y = MFMA64(Is[(16 * Ib + fr) * DW_LD + 16 * Ib + k], Xw[k * 17 + fr], y);
-      }
+      for (int kk = 0; kk < 4; ++kk) y = MFMA64(inv_get(As, 16 * Ib + fr, 16 * Ib + 4 * kk + fk), acc[kk], y);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Is[(16 * Ib + fk + 4 * q) * DW_LD + 16 * Jb + fr] = -y[q];
+      for (int q = 0; q < 4; ++q) inv_at(As, 16 * Ib + fk + 4 * q, 16 * Jb + fr) = -y[q];
     }
     lds_barrier();
   }
 }
 
-__global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict__ cells,
-                                                      const int32_t* __restrict__ list, int j) {
-  __shared__ double As[NB * DW_LD];
-  __shared__ double Is[NB * DW_LD];
-  __shared__ double Xs[4 * 16 * 17];
-  __shared__ double Vs[3 * NB];
-  __shared__ int bad;
-  const OiCell& c = cells[list[blockIdx.x]];
+// LDS of the diagonal factor: As (packed L / Inv) | Vs | sites (j = 0) | bad
+#define DIAG_LDS (NB * DW_LD + 3 * NB + 4 * NB + 2)
+
+// the body of k_diag_factor4w for cell c and tile j: 256 threads work, any
+// larger workgroup passes every barrier with them; `lds` holds DIAG_LDS doubles
+__device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds) {
+  double* As = lds;
+  double* Vs = As + NB * DW_LD;
+  SiteBlk* sb = (SiteBlk*)(Vs + 3 * NB);
+  int& bad = *(int*)(Vs + 7 * NB);
   if (j >= c.T || *c.status != OI_OK) return;
   DIAG_STAMP(0);
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const bool act = t < 256;
   const bool pred = c.mode == OI_MODE_PREDICT;
   double* Y = tileL(c, j, j);
   double* zj = c.vec + j * NB;
@@ -400,7 +409,7 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
       xs1 = (SQRT3 * c.xs[1]) / c.hyp[1];
       xs2 = (SQRT3 * c.xs[2]) / c.hyp[2];
     }
-    for (int a = t; a < c.T * NB; a += 256) {
+    for (int a = t; act && a < c.T * NB; a += 256) {
       const double z = a < n ? c.r[a] : 0.0;
       gst(c.vec + a, z);
       double kv = 0.0;
@@ -418,26 +427,24 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
       }
     }
     // tile (0, 0) generated from the sites (lower triangle; zeros above)
-    SiteBlk* sb = (SiteBlk*)Xs;
-    stage_sites(c, 0, sb, t, 256);
+    if (act) stage_sites(c, 0, sb, t, 256);
     lds_barrier();
     const GenTile A0 = gen_tile(c, sb, 0, sb, 0);
 #pragma unroll 4
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; act && u < 16; ++u) {
       const int e = t + 256 * u, q = e >> 6, r = e & 63;
       As[r * DW_LD + q] = r >= q ? A0(r, q) : 0.0;
-      Is[r * DW_LD + q] = 0.0;
     }
   } else {
     // element (r, q) of the column-major tile at q*64 + r: 16 coalesced loads per
-      // thread; the upper triangle (scratch of the look-ahead) is replaced by zeros
+    // thread; the upper triangle (scratch of the look-ahead) is replaced by zeros
+    if (act)
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = t + 256 * u, q = e >> 6, r = e & 63;
-      const double v = gld(Y + e);
-      As[r * DW_LD + q] = r >= q ? v : 0.0;
-      Is[r * DW_LD + q] = 0.0;
-    }
+      for (int u = 0; u < 16; ++u) {
+        const int e = t + 256 * u, q = e >> 6, r = e & 63;
+        const double v = gld(Y + e);
+        As[r * DW_LD + q] = r >= q ? v : 0.0;
+      }
     if (t < NB) {
       Vs[t] = zj[t];
       Vs[NB + t] = pred ? vj[t] : 0.0;
@@ -459,11 +466,12 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
     return;
   }
   // L_jj (column-major) and sum log L_rr
+  if (act)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int e = t + 256 * u, q = e >> 6, r = e & 63;
-    gst(Y + e, As[r * DW_LD + q]);
-  }
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      gst(Y + e, r >= q ? As[r * DW_LD + q] : 0.0);
+    }
   if (w == 0) {
     double lg = (j * NB + lane < c.n) ? log(As[lane * (DW_LD + 1)]) : 0.0;
     for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
@@ -473,22 +481,23 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
     }
   }
   DIAG_STAMP(3);
-  trtri4w(As, Is, Xs);
+  trtri4w(As, (double*)sb);  // (the j = 0 sites are dead by now)
   DIAG_STAMP(5);
   // Dinv_jj column-major: D[q*64 + r] = Inv[r][q]
   double* Dj = tileD(c, j);
+  if (act)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int e = t + 256 * u, q = e >> 6, r = e & 63;
-    gst(Dj + e, Is[r * DW_LD + q]);
-  }
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+      gst(Dj + e, inv_get(As, r, q));
+    }
   // forward substitution, block j: z_j = Dinv_jj z_j (the panels subtracted the
   // sum over k < j), v_j likewise for predict; z^T z, z^T v, v^T v partials
   if (w == 0) {
     double zp[4] = {0.0, 0.0, 0.0, 0.0}, vp[4] = {0.0, 0.0, 0.0, 0.0};  // four chains
-#pragma unroll
+#pragma unroll 8
     for (int q = 0; q < NB; ++q) {
-      const double a = Is[lane * DW_LD + q];
+      const double a = inv_get(As, lane, q);
       zp[q & 3] = fma(a, Vs[q], zp[q & 3]);
       vp[q & 3] = fma(a, Vs[NB + q], vp[q & 3]);
     }
@@ -513,20 +522,27 @@ __global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict_
   if (c.mode == OI_MODE_EVAL) {
     // W_jj row-major (W[q][r] = Inv[q][r]) and alpha_j = W_jj^T z_j
     double* Wj = tileW(c, j, j);
+    if (act)
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = t + 256 * u;
-      gst(Wj + e, Is[(e >> 6) * DW_LD + (e & 63)]);
-    }
+      for (int u = 0; u < 16; ++u) {
+        const int e = t + 256 * u;
+        gst(Wj + e, inv_get(As, e >> 6, e & 63));
+      }
     lds_barrier();  // z_j in Vs
     if (w == 0) {
       double ap[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int q = 0; q < NB; ++q) ap[q & 3] = fma(Is[q * DW_LD + lane], Vs[2 * NB + q], ap[q & 3]);
+#pragma unroll 8
+      for (int q = 0; q < NB; ++q) ap[q & 3] = fma(inv_get(As, q, lane), Vs[2 * NB + q], ap[q & 3]);
       gst(c.vec + c.T * NB + j * NB + lane, (ap[0] + ap[1]) + (ap[2] + ap[3]));
     }
   }
   DIAG_STAMP(7);
+}
+
+__global__ __launch_bounds__(256) void k_diag_factor4w(const OiCell* __restrict__ cells,
+                                                      const int32_t* __restrict__ list, int j) {
+  __shared__ double lds[DIAG_LDS];
+  diag_tile(cells[list[blockIdx.x]], j, lds);
 }
 
 // wave masks of the GEMM cores (padding, triangular operands, syrk halves): oi_masks.h
@@ -621,6 +637,16 @@ __device__ __forceinline__ void alpha_update(const OiCell& c, const double* X, i
   }
 }
 
+// acc(m, n) = -base[m*64 + n] (the gemm1 accumulator layout)
+__device__ __forceinline__ void acc_load_neg(Quad& acc, const double* base) {
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc.c[mb][nb][r] = -gld(base + acc1_row(mb, r) * NB + acc1_col(nb));
+}
+
 // --------------------------------------------------- k_chol_panel(j)
 // One 256-thread workgroup per output tile; logical slots of a cell:
 //   x <  T-1-j : tile (i = j+1+x, j) of the factor; slot 0 (i = j+1) then
@@ -707,13 +733,7 @@ __device__ __forceinline__ void post_left(const Quad& acc, double* lds, const do
 // (its own instantiation: the generating epilogue would cost the common
 // kbeg = j - 1 launches a wave per SIMD)
 template <bool GEN>
-__global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ cells,
-                                                   const int32_t* __restrict__ list, int j,
-                                                   int kbeg, int gx, int ncell) {
-  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
-  int ci, x;
-  if (!xcd_cell_slot_lead0(gx, ncell, ci, x)) return;
-  const OiCell& c = cells[list[ci]];
+__device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int x, double* lds) {
   const int T = c.T;
   if (j >= T || *c.status != OI_OK) return;
   const int ntrsm = T - 1 - j;
@@ -729,6 +749,10 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
     // n = row of block row i: padding rows of the last block are skipped
     const unsigned psk = i == T - 1 ? pad_skip(32 * wr, 32 * wc, NB, rT) : 0u;
     double* Y = tileL(c, i, j);
+    // the stored A'_ij enters the accumulators before the GEMM (acc = -A'),
+    // so its load overlaps the operand stream instead of following it:
+    // afterwards S = A' - sum = -acc (post_left with no base)
+    if (!GEN) acc_load_neg(acc, Y);
     gemm1_kmajor<true>(acc, lds, 4 * (j - kbeg), psk, [=, &c](int p, const double*& a, const double*& b) {
       a = tileL(c, j, kbeg + p);
       b = tileL(c, i, kbeg + p);
@@ -743,7 +767,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
       const GenTile Aij = gen_tile(c, &sbl[0], i, &sbl[1], j);
       post_left(acc, lds, nullptr, &Aij, Dj, Y);  // L_ij^T = Dinv_jj (A_ij^T - acc), stored and staged
     } else {
-      post_left(acc, lds, Y, nullptr, Dj, Y);
+      post_left(acc, lds, nullptr, nullptr, Dj, Y);
     }
     fwd_update<256>(c, lds, XLD, i, pre, lds + NB * XLD);
     if (x != 0) return;
@@ -787,6 +811,8 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
           const int m = acc1_row(mb, r), n = acc1_col(nb);
           gst(Yd + m * NB + n, Ad(n, m) - accd.c[mb][nb][r]);
         }
+    __syncthreads();
+    diag_tile(c, i, lds);  // the diagonal tile j+1 is final: factor it here
     return;
   }
   const int jj = x - ntrsm;
@@ -798,14 +824,26 @@ __global__ __launch_bounds__(256) void k_chol_panel(const OiCell* __restrict__ c
   // m = row of W block row j: padding rows of the last block are skipped
   const unsigned psk = j == T - 1 ? pad_skip(32 * wr, 32 * wc, rT, NB) : 0u;
   double* Wt = tileW(c, j, jj);
+  if (extra) acc_load_neg(acc, Wt);  // Vneg into the accumulators (as A'_ij above)
   // pair k = jj: B = W_jj,jj (B(k, n) = 0 for k < n)
   auto cm = [=](int ch) { return !extra && ch < 4 ? cols_below(ch, 32 * wc) : 0u; };
   gemm1_kmajor<true>(acc, lds, 4 * (j - kfirst), psk, [=, &c](int p, const double*& a, const double*& b) {
     a = tileL(c, j, kfirst + p);
     b = tileW(c, kfirst + p, jj);
   }, cm);
-  post_left(acc, lds, extra ? Wt : nullptr, nullptr, Dj, Wt);  // W_j,jj = Dinv_jj (Vneg - acc), stored and staged
+  post_left(acc, lds, nullptr, nullptr, Dj, Wt);  // W_j,jj = Dinv_jj (Vneg - sum), stored and staged
   alpha_update<256>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
+}
+
+template <bool GEN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_chol_panel(const OiCell* __restrict__ cells,
+                                                   const int32_t* __restrict__ list, int j,
+                                                   int kbeg, int gx, int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
+  int ci, x;
+  if (!xcd_cell_slot_lead0(gx, ncell, ci, x)) return;
+  chol_slot<GEN>(cells[list[ci]], j, kbeg, x, lds);
 }
 
 // --------------------------------------------------- k_panel_even(j), j even
@@ -1002,6 +1040,8 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
       }
     }
     emit_half(acc, 1, lds, tileL(c, i, i), EMIT_GENSUB, &Ai1);  // i = j+1: A_j+1,j+1 - acc
+    __syncthreads();
+    diag_tile(c, i, lds);  // the diagonal tile j+1 is final: factor it here
     return;
   }
   const int jj = x - ntrsm;
@@ -1232,12 +1272,17 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
       else
         emit_copy(Y, tileL(c, i1, i1), EMIT_GENSUB, &A1n);
     }
-    if (!two) return;
-    __syncthreads();
-    stage_post4(o, 1, lds);  // L_{i2,j}
-    __syncthreads();
-    emit_copy(lds, tileL(c, i2, j), EMIT_STORE);
-    fwd_update<GEMM_THREADS>(c, lds, XLD, i2, pre2, lds + NB * XLD);
+    if (two) {
+      __syncthreads();
+      stage_post4(o, 1, lds);  // L_{i2,j}
+      __syncthreads();
+      emit_copy(lds, tileL(c, i2, j), EMIT_STORE);
+      fwd_update<GEMM_THREADS>(c, lds, XLD, i2, pre2, lds + NB * XLD);
+    }
+    if (x == 0) {  // the diagonal tile j+1 is final: factor it here (no k_diag_factor4w launch)
+      __syncthreads();
+      diag_tile(c, i1, lds);
+    }
     return;
   }
   const int y = x - nfp;
@@ -1293,13 +1338,7 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
 // sum over the tile of (K^-1 - alpha alpha^T) o {dK_0, dK_1, dK_2, 2K} and the
 // trace (GPR:130-138); K and dK are regenerated from the coordinates.
 // Strictly-lower entries count twice.
-__global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ cells,
-                                                    const int32_t* __restrict__ list, int gx,
-                                                    int ncell) {
-  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
-  int ci, tile;
-  if (!xcd_cell_slot(gx, ncell, ci, tile)) return;
-  const OiCell& c = cells[list[ci]];
+__device__ __forceinline__ void lauum_tile(const OiCell& c, int tile, double* lds) {
   const int T = c.T;
   int i, j;
   if (!decode_tri(tile, T, i, j)) return;
@@ -1385,6 +1424,15 @@ __global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ 
     double* pp = c.part + OI_PART_GRAD(0) + 5 * (size_t)tile;
     for (int q = 0; q < 5; ++q) pp[q] = s[q];
   }
+}
+
+__global__ __launch_bounds__(256) void k_lauum_grad1(const OiCell* __restrict__ cells,
+                                                    const int32_t* __restrict__ list, int gx,
+                                                    int ncell) {
+  __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
+  int ci, tile;
+  if (!xcd_cell_slot(gx, ncell, ci, tile)) return;
+  lauum_tile(cells[list[ci]], tile, lds);
 }
 
 // ---------------------------------------------------------- k_finalize

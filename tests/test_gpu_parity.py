@@ -364,5 +364,10 @@ def test_profile_by_j_matches_kernel_totals():
         assert abs(sum(r[4] for r in rows) - v['total_ms']) <= 1e-3 * max(1.0, v['total_ms']), k
         if v['flops'] > 0 and k != 'k_lauum_grad':
             assert abs(sum(r[5] for r in rows) - v['flops']) <= 1e-6 * v['flops'], k  # printed to 7 digits
-    js = sorted(r[1] for r in byj if r[0] == 'k_diag_factor')   # one row per block column 0 .. T-1
-    assert js == list(range(len(js))) and len(js) >= 2
+    # k_diag_factor4w runs for block column 0 only: the look-ahead workgroup of
+    # column j's panel launch factors diagonal tile j+1 (round 5)
+    js = sorted(r[1] for r in byj if r[0] == 'k_diag_factor')
+    assert js == [0]
+    jp = sorted({r[1] for r in byj if r[0] in ('k_panel4', 'k_panel_even', 'k_chol_panel')})
+    assert jp == list(range(len(jp))) and len(jp) >= 2
+
