@@ -17,7 +17,7 @@
 
 namespace oila {
 
-struct LinalgErr {  // thrown by the host routines on a HIP error
+struct LinalgErr {  // thrown by the host routines on a HIP error or an operand too large
   std::string msg;
 };
 
@@ -45,12 +45,16 @@ struct Gemv {
 
 // One symmetric matrix for the eigensolver: A (M x M, lower triangle read;
 // destroyed, then overwritten with the eigenvectors), w (M eigenvalues,
-// ascending), and its workspace (workspace_doubles(M) doubles).
+// ascending), its workspace (workspace_doubles(M) doubles), and info (device,
+// may be null): set to 1 -- LAPACK syevd's info > 0, numpy's LinAlgError --
+// when the orthogonalisation cannot produce a finite column in its four
+// attempts; left untouched otherwise (NaN input propagates as NaN).
 struct Eigh {
   double* A;
   double* w;
   double* work;
   int M, lda;
+  int* info;
 };
 size_t eigh_workspace_doubles(int M);
 

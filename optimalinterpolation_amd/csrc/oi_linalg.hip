@@ -836,6 +836,7 @@ __global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es,
   };
   for (int j = p; j < q; ++j) {
     gdouble* zj = Z + ld * j;
+    bool done = false, nan = false;
     for (int attempt = 0; attempt < 4; ++attempt) {
       const int lo = attempt == 0 ? p : 0;  // a fresh vector is projected out of everything
       double dv[33];
@@ -871,15 +872,21 @@ __global__ __launch_bounds__(MG_T) void k_mgs_panel(const Eigh* __restrict__ es,
       for (int i = t; i < M; i += MG_T) dv[32] += zj[i] * zj[i];
       reduce(dv);
       const double n1 = dv[32];
+      nan = nan || !(n0 == n0) || !(n1 == n1);
       if (n1 > 1e-4 * n0 && n1 > 0.0) {
         const double inv = 1.0 / sqrt(n1);
         for (int i = t; i < M; i += MG_T) zj[i] *= inv;
         __syncthreads();
+        done = true;
         break;
       }
       for (int i = t; i < M; i += MG_T) zj[i] = start_value(j + 7919 * (attempt + 1), i);
       __syncthreads();
     }
+    // four collapses in a row of a finite column: it is not an orthonormal
+    // vector (reported like a non-converged syevd).  NaN input
+    // propagates instead, as numpy's eigh does when LAPACK returns NaNs.
+    if (!done && !nan && t == 0 && E.info) *E.info = 1;
   }
 }
 
@@ -1042,14 +1049,29 @@ const void* Stager::put_bytes(const void* p, size_t bytes) {
   return d;
 }
 
+// bload's descriptors cover 0x7FFFFFF0 bytes from an operand's base and take
+// 32-bit byte offsets: an operand whose stored extent reaches past that would
+// wrap or read zeros instead of failing, so the wrappers refuse it
+static void check_extent(int64_t ld, int64_t rows, int64_t cols, const char* what) {
+  if (rows <= 0 || cols <= 0) return;
+  if ((ld * (cols - 1) + rows) * 8 >= (int64_t)0x7FFFFFF0)
+    throw LinalgErr{std::string(what) + ": operand extent >= 2 GiB (32-bit buffer offsets)"};
+}
+
 void gemm(Stager& S, hipStream_t st, bool ta, bool tb, const std::vector<Gemm>& g) {
   std::vector<Gemm> live;
   int tiles = 0;
-  for (const Gemm& x : g)
+  for (const Gemm& x : g) {
+    if (x.m > 0 && x.n > 0 && x.k > 0) {
+      check_extent(x.lda, ta ? x.k : x.m, ta ? x.m : x.k, "gemm A");
+      check_extent(x.ldb, tb ? x.n : x.k, tb ? x.k : x.n, "gemm B");
+      check_extent(x.ldc, x.m, x.n, "gemm C");
+    }
     if (x.m > 0 && x.n > 0) {
       live.push_back(x);
       tiles = std::max(tiles, ((x.m + GT - 1) / GT) * ((x.n + GT - 1) / GT));
     }
+  }
   if (live.empty()) return;
   const Gemm* dg = S.put(live);
   dim3 grid((unsigned)tiles, (unsigned)live.size());
@@ -1065,6 +1087,7 @@ void gemv(Stager& S, hipStream_t st, bool trans, const std::vector<Gemv>& g) {
   int outs = 0;
   for (const Gemv& x : g)
     if (x.m > 0 && x.n > 0) {
+      check_extent(x.lda, x.m, x.n, "gemv A");
       live.push_back(x);
       outs = std::max(outs, trans ? x.n : x.m);
     }
@@ -1081,7 +1104,10 @@ void gemv(Stager& S, hipStream_t st, bool trans, const std::vector<Gemv>& g) {
 void cholesky(Stager& S, hipStream_t st, const std::vector<Chol>& cs) {
   if (cs.empty()) return;
   int Mmax = 0;
-  for (const Chol& c : cs) Mmax = std::max(Mmax, c.M);
+  for (const Chol& c : cs) {
+    Mmax = std::max(Mmax, c.M);
+    check_extent(c.lda, c.M, c.M, "cholesky A");
+  }
   const Chol* dc = S.put(cs);
   for (int jb = 0; jb < Mmax; jb += 64) {
     hipLaunchKernelGGL(k_potrf_tile, dim3((unsigned)cs.size()), dim3(64), 0, st, dc, jb);
@@ -1128,7 +1154,10 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
     if (mark) mark(k);
   };
   int Mmax = 0;
-  for (const Eigh& e : es) Mmax = std::max(Mmax, e.M);
+  for (const Eigh& e : es) {
+    Mmax = std::max(Mmax, e.M);
+    check_extent(e.lda, e.M, e.M, "eigh A");
+  }
   if (Mmax > 4096) throw LinalgErr{"eigh: M > 4096 not supported"};
   const Eigh* de = S.put(es);
   const unsigned n = (unsigned)es.size();

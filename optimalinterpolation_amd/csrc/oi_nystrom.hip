@@ -790,7 +790,8 @@ class Runner {
         std::vector<oila::Eigh> es;
         for (int q = 0; q < cnt; ++q)
           es.push_back(oila::Eigh{Kmm_.as<double>() + (s0 + q) * mm, eval_.as<double>() + (s0 + q) * mpmax_,
-                                  EW_.as<double>() + (s0 + q) * ewd_, iM, iM});
+                                  EW_.as<double>() + (s0 + q) * ewd_, iM, iM,
+                                  info_.as<int32_t>() + (g0 + q) * NINFO + 0});
         // algorithmic flops per phase: tridiagonalisation 4/3 M^3, tridiagonal
         // eigenpairs O(M^2), BCGS2 2 M^3, back-transform 2 M^3
         const double m3 = dM * dM * dM * cnt;
@@ -1277,7 +1278,11 @@ struct NysTicket {
 struct oi_nystrom_session {
   oi_options o;
   int G = 2;
-  int64_t cap = 32;  // resident fitting cells per group
+  // resident fitting cells per group (OI_NYS_CAP): the batched eigensolver's
+  // per-column launches cost the same for 32 or 64 matrices, so a bigger chunk
+  // amortises them -- 5.46 / 6.69 / 6.63 cells/s at 32 / 64 / 128
+  // (--workload nystrom, one box, profiles/r05/nystrom_cap/)
+  int64_t cap = 64;
   int32_t maxiter = 1000;
   double gtol = 1e-5;
   std::vector<CellSrc> tab;          // every submitted cell, by global id
