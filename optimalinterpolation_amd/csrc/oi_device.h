@@ -89,13 +89,15 @@ extern "C" {
 // kernel launchers (oi_kernels.hip); `cells` and `list` are device pointers,
 // `list` holds indices into `cells` sorted by T descending.
 int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, int ncell, int j, void* stream);
-// the panels stream the L tiles and apply Dinv_jj to the finished sum (post-form)
+// the panels stream the L tiles and apply Dinv_jj to the finished sum (post-form);
+// fuse_diag: the look-ahead workgroup also factors diagonal tile j+1 (else
+// oi_launch_diag_factor(j+1) follows)
 int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                         int kbeg, int with_trtri, void* stream);
+                         int kbeg, int with_trtri, int fuse_diag, void* stream);
 int oi_launch_panel4(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j, int with_trtri,
-                     void* stream);
+                     int fuse_diag, void* stream);
 int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                         int with_trtri, void* stream);
+                         int with_trtri, int fuse_diag, void* stream);
 int oi_launch_lauum_grad(const OiCell* cells, const int32_t* list, int ncell, int maxT,
                          void* stream);
 // flag != nullptr: the last workgroup stores seq to *flag (pinned host) once all

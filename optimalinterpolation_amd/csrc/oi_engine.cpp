@@ -159,6 +159,19 @@ int panel4_mint() {
   const char* e = getenv("OI_PANEL4_MINT");
   return e ? atoi(e) : 12;
 }
+// ... and only when the launch has at least OI_PANEL4_MINWG (512: two
+// k_panel4 workgroups per CU) workgroups -- the day's tail rounds of a few
+// slow-converging cells run the one-row kernel, twice as many workgroups
+int panel4_minwg() {
+  const char* e = getenv("OI_PANEL4_MINWG");
+  return e ? atoi(e) : 512;
+}
+// rounds of at least OI_FUSE_DIAG_MIN cells factor diagonal tile j+1 inside
+// column j's panel launch (k_diag_factor4w then runs for column 0 only)
+int fuse_diag_min() {
+  const char* e = getenv("OI_FUSE_DIAG_MIN");
+  return e ? atoi(e) : 1;
+}
 // Executed MFMA flops per cell and launch (profile mode), mirroring the
 // kernels' wave masks (oi_masks.h): a 16x16 accumulator block over one
 // 16-deep k-chunk is 8192 flops.  gemm2 (k_panel_even: 8 waves, wr 0..1,
@@ -532,7 +545,8 @@ class Engine {
  public:
   Engine(Context& ctx, const oi_options& o, int64_t cap_hint)
       : ctx_(ctx), o_(o), legacy_(legacy_panels()), panel4_(panel4_enabled()),
-        panel4_minj_(panel4_minj()), panel4_mint_(panel4_mint()) {
+        panel4_minj_(panel4_minj()), panel4_mint_(panel4_mint()), panel4_minwg_(panel4_minwg()),
+        fuse_diag_min_(fuse_diag_min()) {
     HIPC(hipSetDevice(ctx.device));
     st_ = o.stream ? (hipStream_t)o.stream : ctx.own_stream;
     ss_ = ctx.sub_stream;
@@ -717,8 +731,13 @@ class Engine {
   bool done(int64_t id) const { return id < next_id_ && !jobs_.count(id); }
 
 
-  bool use_panel4(int j, int maxT) const {
-    return panel4_ && j >= panel4_minj_ && maxT >= panel4_mint_;
+  // k_panel4 (two block rows per 512-thread workgroup) when the launch still
+  // fills the chip, else k_panel_even (one block row: twice the workgroups);
+  // the two are bitwise equal (round 5), so the choice never changes a result
+  bool use_panel4(int j, int maxT, int cnt, bool trtri) const {
+    if (!(panel4_ && j >= panel4_minj_ && maxT >= panel4_mint_)) return false;
+    const int64_t wg = (int64_t)cnt * (((maxT - j) >> 1) + (trtri ? j / 2 : 0));
+    return wg >= panel4_minwg_;
   }
 
   // The stream later submissions' device inputs are ordered after (the rounds
@@ -925,8 +944,12 @@ class Engine {
       cur_j = j;
       cur_cells = cnt;
       // diagonal tile 0 has its own launch; tile j+1 is factored by the
-      // look-ahead workgroup of column j's panel launch (round 5)
-      if (j == 0) {
+      // look-ahead workgroup of column j's panel launch (round 5) -- unless the
+      // round holds fewer than OI_FUSE_DIAG_MIN cells (the lone cell of config
+      // 1: there a launch of its own is cheaper than the long look-ahead
+      // workgroup); bitwise the same either way
+      const bool fuse = na >= fuse_diag_min_;
+      if (j == 0 || !fuse) {
         mark(K_CHOL, false);
         rc |= oi_launch_diag_factor(dc, dl_all, cnt, j, gst);
         mark(K_CHOL, true);
@@ -938,16 +961,16 @@ class Engine {
       const bool empty_panel = j == maxT - 1 && ne == 0;
       if (empty_panel) {
       } else if (even) {
-        const int ke = use_panel4(j, maxT) ? K_EVEN4 : K_EVEN;
+        const int ke = use_panel4(j, maxT, cnt, ne > 0) ? K_EVEN4 : K_EVEN;
         mark(ke, false);
         if (ke == K_EVEN4)
-          rc |= oi_launch_panel4(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
+          rc |= oi_launch_panel4(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, fuse, gst);
         else
-          rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, gst);
+          rc |= oi_launch_panel_even(dc, dl_all, cnt, maxT, j, ne > 0 ? 1 : 0, fuse, gst);
         mark(ke, true);
       } else {
         mark(K_TRSM, false);
-        rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, gst);
+        rc |= oi_launch_chol_panel(dc, dl_all, cnt, maxT, j, kbeg, ne > 0 ? 1 : 0, fuse, gst);
         mark(K_TRSM, true);
       }
       if (o_.profile) {  // executed MFMA flops, mirroring the kernels' masks (acct::)
@@ -955,7 +978,7 @@ class Engine {
           const OiCell& cd = hc(all_slots[k]);
           const bool ev = cd.mode == OI_MODE_EVAL;
           if (empty_panel) continue;
-          const int kk = even ? (use_panel4(j, maxT) ? K_EVEN4 : K_EVEN) : K_TRSM;
+          const int kk = even ? (use_panel4(j, maxT, cnt, ne > 0) ? K_EVEN4 : K_EVEN) : K_TRSM;
           const double f = kk == K_EVEN4 ? acct::panel4(cd.T, cd.n, j, ev)
                            : kk == K_EVEN ? acct::panel_even(cd.T, cd.n, j, ev, true)
                                           : acct::chol_panel(cd.T, cd.n, j, kbeg, ev, true);
@@ -1137,7 +1160,7 @@ class Engine {
   Context& ctx_;
   oi_options o_;
   bool legacy_ = false, poison_ = false, panel4_ = false;
-  int panel4_minj_ = 0, panel4_mint_ = 12;
+  int panel4_minj_ = 0, panel4_mint_ = 12, panel4_minwg_ = 512, fuse_diag_min_ = 1;
   hipStream_t st_ = nullptr, ss_ = nullptr;
   hipEvent_t ready_ = nullptr;
   int cap_ = 1, G_ = 1, capG_ = 1;

@@ -733,7 +733,7 @@ __device__ __forceinline__ void post_left(const Quad& acc, double* lds, const do
 // (its own instantiation: the generating epilogue would cost the common
 // kbeg = j - 1 launches a wave per SIMD)
 template <bool GEN>
-__device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int x, double* lds) {
+__device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int x, double* lds, int fuse) {
   const int T = c.T;
   if (j >= T || *c.status != OI_OK) return;
   const int ntrsm = T - 1 - j;
@@ -811,8 +811,10 @@ __device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int 
           const int m = acc1_row(mb, r), n = acc1_col(nb);
           gst(Yd + m * NB + n, Ad(n, m) - accd.c[mb][nb][r]);
         }
-    __syncthreads();
-    diag_tile(c, i, lds);  // the diagonal tile j+1 is final: factor it here
+    if (fuse) {  // the diagonal tile j+1 is final: factor it here
+      __syncthreads();
+      diag_tile(c, i, lds);
+    }
     return;
   }
   const int jj = x - ntrsm;
@@ -839,11 +841,11 @@ template <bool GEN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_chol_panel(const OiCell* __restrict__ cells,
                                                    const int32_t* __restrict__ list, int j,
-                                                   int kbeg, int gx, int ncell) {
+                                                   int kbeg, int gx, int ncell, int fuse) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
   int ci, x;
   if (!xcd_cell_slot_lead0(gx, ncell, ci, x)) return;
-  chol_slot<GEN>(cells[list[ci]], j, kbeg, x, lds);
+  chol_slot<GEN>(cells[list[ci]], j, kbeg, x, lds, fuse);
 }
 
 // --------------------------------------------------- k_panel_even(j), j even
@@ -974,7 +976,7 @@ __device__ __forceinline__ void post_right(const Quad& acc, double* lds, const G
 
 __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __restrict__ cells,
                                                             const int32_t* __restrict__ list,
-                                                            int j, int gx, int ncell) {
+                                                            int j, int gx, int ncell, int fuse) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
   __shared__ SiteBlk sb[3];  // sites of block row i, block columns j, j+1
   static_assert(NB * XLD <= GEMM2_LDS, "staging tile must fit the GEMM LDS");
@@ -1011,6 +1013,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
     }, sk);
     if (j == 0) __syncthreads();  // no GEMM ran: the staged sites need a barrier
     const GenTile Aij = gen_tile(c, &sb[0], i, &sb[1], j), Ai1 = gen_tile(c, &sb[0], i, &sb[2], j + 1);
+    // (x = 0: half 1 is the diagonal tile j+1; it is completed below as
+    // (A - acc) - L_j+1,j L_j+1,j^T -- the look-ahead arithmetic of k_panel4,
+    // so the two even-column kernels agree bit for bit and the engine may pick
+    // either per round, round 5)
     post_right(acc, lds, &Aij, Dj);  // L_ij = (A_ij - acc) Dinv_jj^T, staged
     emit_copy(lds, tileL(c, i, j), EMIT_STORE);
     fwd_update<GEMM_THREADS>(c, lds, XLD, i, pre, lds + NB * XLD);
@@ -1019,8 +1025,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
       if (j > 0) emit_half(acc, 1, lds, tileL(c, i, j + 1), EMIT_GENSUB, &Ai1);
       return;
     }
-    // i = j+1: add the fresh L_j+1,j L_j+1,j^T (staged in lds as X[q*XLD + m] =
-    // L[m][q]) to the half-1 accumulator, then complete A_j+1,j+1.
+    // i = j+1: the fresh L_j+1,j L_j+1,j^T (staged in lds as X[q*XLD + m] =
+    // L[m][q]) in zeroed accumulators; then A_j+1,j+1 - acc and that minus it
+    Quad lf;
+    quad_zero(lf);
     __syncthreads();
     {
       const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1032,16 +1040,19 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __res
           const int q = kk * 4 + fk;
           const double a0 = lds[q * XLD + 32 * wr + fr], a1 = lds[q * XLD + 32 * wr + 16 + fr];
           const double b0 = lds[q * XLD + c0 + fr], b1 = lds[q * XLD + c0 + 16 + fr];
-          acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
-          acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
-          acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
-          acc.c[1][1] = MFMA64(a1, b1, acc.c[1][1]);
+          lf.c[0][0] = MFMA64(a0, b0, lf.c[0][0]);
+          lf.c[0][1] = MFMA64(a0, b1, lf.c[0][1]);
+          lf.c[1][0] = MFMA64(a1, b0, lf.c[1][0]);
+          lf.c[1][1] = MFMA64(a1, b1, lf.c[1][1]);
         }
       }
     }
-    emit_half(acc, 1, lds, tileL(c, i, i), EMIT_GENSUB, &Ai1);  // i = j+1: A_j+1,j+1 - acc
-    __syncthreads();
-    diag_tile(c, i, lds);  // the diagonal tile j+1 is final: factor it here
+    emit_half(acc, 1, lds, tileL(c, i, i), EMIT_GENSUB, &Ai1);
+    emit_half(lf, 1, lds, tileL(c, i, i), EMIT_SUB);  // (A_j+1,j+1 - acc) - L L^T
+    if (fuse) {  // the diagonal tile j+1 is final: factor it here
+      __syncthreads();
+      diag_tile(c, i, lds);
+    }
     return;
   }
   const int jj = x - ntrsm;
@@ -1178,7 +1189,8 @@ __device__ __forceinline__ void stage_post4(const d4 (&o)[2][2], int r, double* 
 }
 
 __global__ __launch_bounds__(GEMM_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list, int j, int gx, int ncell) {
+void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list, int j, int gx, int ncell,
+              int fuse) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM4_LDS];
   __shared__ SiteBlk sb[4];  // sites of block rows i1, i2 and block columns j, j+1 (80 KiB in all: 2 per CU)
   static_assert(2 * NB * SLD <= GEMM4_LDS && 2 * NB * XLD <= GEMM4_LDS, "panel4 staging must fit");
@@ -1279,7 +1291,7 @@ void k_panel4(const OiCell* __restrict__ cells, const int32_t* __restrict__ list
       emit_copy(lds, tileL(c, i2, j), EMIT_STORE);
       fwd_update<GEMM_THREADS>(c, lds, XLD, i2, pre2, lds + NB * XLD);
     }
-    if (x == 0) {  // the diagonal tile j+1 is final: factor it here (no k_diag_factor4w launch)
+    if (x == 0 && fuse) {  // the diagonal tile j+1 is final: factor it here (no k_diag_factor4w launch)
       __syncthreads();
       diag_tile(c, i1, lds);
     }
@@ -1670,33 +1682,33 @@ extern "C" int oi_launch_diag_factor(const OiCell* cells, const int32_t* list, i
 }
 
 extern "C" int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                                    int j, int kbeg, int with_trtri, void* stream) {
+                                    int j, int kbeg, int with_trtri, int fuse_diag, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
   if (kbeg == 0)
     hipLaunchKernelGGL(k_chol_panel<true>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, kbeg,
-                       gx, ncell);
+                       gx, ncell, fuse_diag);
   else
     hipLaunchKernelGGL(k_chol_panel<false>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, kbeg,
-                       gx, ncell);
+                       gx, ncell, fuse_diag);
   return ret();
 }
 
 extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, int ncell, int maxT,
-                                    int j, int with_trtri, void* stream) {
+                                    int j, int with_trtri, int fuse_diag, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
   hipLaunchKernelGGL(k_panel_even, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j, gx,
-                     ncell);
+                     ncell, fuse_diag);
   return ret();
 }
 
 extern "C" int oi_launch_panel4(const OiCell* cells, const int32_t* list, int ncell, int maxT, int j,
-                                int with_trtri, void* stream) {
+                                int with_trtri, int fuse_diag, void* stream) {
   const int gx = nslot4_factor(maxT, j) + (with_trtri ? j / 2 : 0);
   if (ncell <= 0 || gx <= 0) return 0;
   hipLaunchKernelGGL(k_panel4, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j, gx,
-                     ncell);
+                     ncell, fuse_diag);
   return ret();
 }
 

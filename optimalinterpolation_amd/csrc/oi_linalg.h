@@ -61,7 +61,8 @@ size_t eigh_workspace_doubles(int M);
 // One SPD matrix for the blocked Cholesky: A (M x M, lower triangle; the
 // factor L overwrites it), dinv (ceil(M/64) x 4096 doubles: the inverses of
 // L's 64 x 64 diagonal blocks, kept for trsm_right_lt), info (0, or 1 when
-// a pivot is <= 0 or NaN, as LAPACK dpotrf's info > 0).
+// a pivot is <= 0, as LAPACK dpotrf's info > 0; a NaN pivot propagates, as
+// numpy + OpenBLAS's dpotrf let it).
 struct Chol {
   double* A;
   double* dinv;

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64) void k_potrf_tile(const Chol* __restrict__ cs, 
   bool bad = false;
   for (int j = 0; j < nb; ++j) {
     const double p = L[j * 65 + j];
-    if (!(p > 0.0)) bad = true;
+    if (p <= 0.0) bad = true;  // a NaN pivot propagates (numpy + OpenBLAS's dpotrf do not flag it)
     const double ljj = sqrt(p);
     __syncthreads();
     if (r == j) L[j * 65 + j] = ljj;

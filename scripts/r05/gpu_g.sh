@@ -3,7 +3,7 @@
 # session, days in order; parity block of the timed cells
 set -o pipefail
 D=gpurun_out/r05/g; mkdir -p $D
-timeout -k 10 1150 python3 bench.py --workload season --season-days 3 --steps 21 --warmup 2 --budget-s 1050 --no-cpu-baseline --out $D/season_3days.json > $D/season_3days.log 2>&1 || { tail -20 $D/season_3days.log; exit 1; }
+timeout -k 10 1150 python3 bench.py --workload season --season-days 3 --steps 21 --warmup 2 --budget-s 1000 --no-cpu-baseline --parity-cells 8 --out $D/season_3days.json > $D/season_3days.log 2>&1 || { tail -20 $D/season_3days.log; exit 1; }
 python3 -c "
 import json; d=json.load(open('$D/season_3days.json')); r=d['roofline']
 print('season 3 days', d['value'], d['timed_s'], d.get('truncated'), d['config']['cells_total'], d['evals_per_cell'], r['kernel'], r['frac'], d['parity'])"

@@ -315,18 +315,19 @@ def test_duplicate_nonpd_band():
 def test_panel4_equals_panel_even(monkeypatch):
     """k_panel4 (two block rows per workgroup on the 128 x 128 core) does the
     even-column panel's arithmetic in the same order as k_panel_even (same
-    MFMA chunk sequence, S = A - acc, the same triangular product) except the
-    look-ahead diagonal tile, (A - acc) - L L^T instead of A - (acc + L L^T):
-    objective, gradient and predictions agree to rounding (1e-12 relative),
-    poisoned workspaces (OI_POISON=1) included -- nothing is read before it
-    is written -- and each variant is bitwise reproducible."""
+    MFMA chunk sequence, S = A - acc, the same triangular product, and since
+    round 5 the same look-ahead, (A - acc) - L L^T): objective, gradient and
+    predictions are BITWISE equal, so the engine's per-round choice between
+    them never changes a result; poisoned workspaces (OI_POISON=1) included --
+    nothing is read before it is written."""
     sizes = [1, 40, 63, 64, 65, 128, 129, 191, 192, 193, 257, 700, 1100, 2000]
     cells = synthetic.make_cells(sizes, seed=23)
     h = np.tile(np.array([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(1e-3), 0.]), (len(sizes), 1))
     mX = np.full(len(cells.z), cells.mean)
     hyp = np.tile(synthetic.FIXED_HYPERS, (len(sizes), 1))
     res = {}
-    monkeypatch.setenv('OI_PANEL4_MINT', '0')   # k_panel4 in every round (default: rounds with T >= 12)
+    monkeypatch.setenv('OI_PANEL4_MINT', '0')   # k_panel4 in every round (default: rounds with T >= 12
+    monkeypatch.setenv('OI_PANEL4_MINWG', '0')  # and >= 512 workgroups)
     for p4 in ('0', '1'):
         for poison in ('0', '1'):
             monkeypatch.setenv('OI_PANEL4', p4)
@@ -338,7 +339,29 @@ def test_panel4_equals_panel_even(monkeypatch):
         for a, b in zip(res[(p4, '1')], res[(p4, '0')]):
             assert np.array_equal(a, b), p4
     for a, b in zip(res[('1', '0')], res[('0', '0')]):
-        assert np.all(np.abs(a - b) <= 1e-12 * np.maximum(1.0, np.abs(b))), np.max(np.abs(a - b) / np.maximum(1, np.abs(b)))
+        assert np.array_equal(a, b), np.max(np.abs(a - b) / np.maximum(1, np.abs(b)))
+
+
+def test_cell_result_independent_of_round_mates(monkeypatch):
+    """A cell's results never depend on the other cells of its rounds: small
+    cells (T < 12, k_panel_even when alone) fitted and evaluated alone, and
+    together with large cells (rounds of T >= 12 where the engine may pick
+    k_panel4), are bitwise equal -- objective, gradient, a full opt=True fit
+    and predictions."""
+    monkeypatch.setenv('OI_PANEL4_MINWG', '0')  # the mixed rounds do take k_panel4
+    small = synthetic.make_cells([90, 333, 700], seed=51)
+    big = synthetic.make_cells([1500, 2200], seed=52)
+    both = synthetic.RaggedCells(np.concatenate([small.xyt, big.xyt]), np.concatenate([small.z, big.z]),
+                                 np.concatenate([small.offs, small.offs[-1] + big.offs[1:]]),
+                                 np.concatenate([small.xs, big.xs]), small.mean)
+    h = np.tile(np.array([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(1e-3), 0.]), (5, 1))
+    n1, g1, _ = _lib.nlml_grad_batch(small.xyt, small.z, np.full(len(small.z), small.mean), small.offs, h[:3])
+    n2, g2, _ = _lib.nlml_grad_batch(both.xyt, both.z, np.full(len(both.z), both.mean), both.offs, h)
+    assert np.array_equal(n1, n2[:3]) and np.array_equal(g1, g2[:3])
+    x0 = np.array(O.X0_PRODUCTION)
+    o1, s1, i1 = _lib.gpr_batch(small.xyt, small.z, small.offs, small.xs, small.mean, x0=x0, opt=True, info=True)
+    o2, s2, i2 = _lib.gpr_batch(both.xyt, both.z, both.offs, both.xs, both.mean, x0=x0, opt=True, info=True)
+    assert np.array_equal(o1, o2[:3], equal_nan=True) and np.array_equal(i1, i2[:3])
 
 
 def test_profile_by_j_matches_kernel_totals():
