@@ -313,7 +313,10 @@ __device__ __forceinline__ double potrf4w(double* As) {
 // workgroup of every panel launch factors the next diagonal tile itself).
 __device__ __forceinline__ double& inv_at(double* As, int R, int C) { return As[C * DW_LD + R + 1]; }
 __device__ __forceinline__ double inv_get(const double* As, int R, int C) {
-  return R >= C ? As[C * DW_LD + R + 1] : 0.0;
+  // an unconditional read (row C, column R + 1 <= 64 always exists) masked to 0
+  // above the diagonal: a `R >= C ? load : 0` compiled to exec-masked loads
+  const unsigned long long v = __builtin_bit_cast(unsigned long long, As[C * DW_LD + R + 1]);
+  return __builtin_bit_cast(double, R >= C ? v : 0ull);
 }
 
 // Inv <- L^-1 of the factored tile in As (packed, above); waves 0..3 work, every
@@ -495,7 +498,7 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds) {
   // sum over k < j), v_j likewise for predict; z^T z, z^T v, v^T v partials
   if (w == 0) {
     double zp[4] = {0.0, 0.0, 0.0, 0.0}, vp[4] = {0.0, 0.0, 0.0, 0.0};  // four chains
-#pragma unroll 8
+#pragma unroll 8  // (full unrolling hoists all 64 packed reads: 255 VGPRs; 8 and 16 measured equal)
     for (int q = 0; q < NB; ++q) {
       const double a = inv_get(As, lane, q);
       zp[q & 3] = fma(a, Vs[q], zp[q & 3]);
@@ -974,7 +977,8 @@ __device__ __forceinline__ void post_right(const Quad& acc, double* lds, const G
   __syncthreads();
 }
 
-__global__ __launch_bounds__(GEMM_THREADS) void k_panel_even(const OiCell* __restrict__ cells,
+__global__ __launch_bounds__(GEMM_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_panel_even(const OiCell* __restrict__ cells,
                                                             const int32_t* __restrict__ list,
                                                             int j, int gx, int ncell, int fuse) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];

@@ -330,9 +330,10 @@ __device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] =
 // symv workgroups per matrix: gridDim.y of k_sy_symv (OI_SY_S, default below)
 #define SY_S_DEFAULT 8
 #define SY_S_MAX TNB  // the partials live in the M x 32 H block
-__global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es, int p, int i) {
-  __shared__ double red[64];
-  const Eigh E = es[blockIdx.x];
+// column g = p + i: brought up to date with the panel's earlier reflectors,
+// then its reflector (the body of k_sy_reflect; k_sy_w(i) also runs it for
+// column i + 1, which saves one launch per column)
+__device__ __forceinline__ void sy_reflect(const Eigh& E, int p, int i, double* red) {
   const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i;
   if (p >= M - 1) {
     if (p == 0 && i == 0 && t == 0) ws_d0(E);  // M == 1
@@ -387,6 +388,12 @@ __global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es
     ws.e[g] = beta;
     ws.tau[g] = tau;
   }
+}
+
+__global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es, int p, int i) {
+  __shared__ double red[64];
+  const Eigh E = es[blockIdx.x];
+  sy_reflect(E, p, i, red);
 }
 
 // partial y of workgroup s into H[s M + r] (rows g+1 .. M-1); the panel dots
@@ -479,7 +486,7 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
   }
 }
 
-__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i, int ns) {
+__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i, int ns, int next) {
   __shared__ double red[64];
   __shared__ double pan[2 * TNB];
   const Eigh E = es[blockIdx.x];
@@ -549,6 +556,10 @@ __global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int 
       wcol[ra] = wr2[0][nsw] + a2 * vgc[ra];
       if (rb < M) wcol[rb] = wr2[1][nsw] + a2 * vgc[rb];
     }
+  }
+  if (next) {  // the panel's next column (w column i is visible to the workgroup)
+    __syncthreads();
+    sy_reflect(E, p, i + 1, red);
   }
 }
 
@@ -1174,9 +1185,11 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   // batched GEMMs over the whole chip
   for (int p = 0; p < std::max(Mmax - 1, 1); p += TNB) {
     for (int i = 0; i < TNB && (i == 0 || p + i < Mmax - 1); ++i) {
-      hipLaunchKernelGGL(k_sy_reflect, dim3(n), dim3(SY_T), 0, st, de, p, i);
+      // the panel's first reflector has a launch of its own; k_sy_w(i) forms the next
+      if (i == 0) hipLaunchKernelGGL(k_sy_reflect, dim3(n), dim3(SY_T), 0, st, de, p, i);
       hipLaunchKernelGGL(k_sy_symv, dim3(n, ns), dim3(SY_T), lds_sy, st, de, p, i);
-      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i, ns);
+      const int next = i + 1 < TNB && p + i + 1 < Mmax - 1;
+      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i, ns, next);
     }
     LC(hipGetLastError());
     std::vector<Gemm> g1, g2;
