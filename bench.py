@@ -105,7 +105,7 @@ def parse():
     p.add_argument('--cpu-cores', type=int, default=0,
                    help='CPU baseline worker processes; 0: the host cores this process may use')
     p.add_argument('--timed-profile', default='auto', choices=['auto', 'on', 'off'],
-                   help='per-launch HIP events inside the timed region (auto: on for day/days; off for '
+                   help='per-launch HIP events inside the timed region (auto: on for day/days/season; off for '
                         'single/predict, whose roofline then comes from a second, profiled pass)')
     p.add_argument('--parity-cells', type=int, default=24,
                    help='day workloads: timed cells re-checked against the CPU oracle at the GPU fit\'s '
@@ -1051,7 +1051,8 @@ def main():
         _lib.gpr_batch(prime.xyt, prime.z, prime.offs, prime.xs, prime.mean, x0=X0, opt=True, device=gpu,
                        profile=True)
     single = args.workload == 'single'
-    tprof = (args.workload in ('day', 'days')) if args.timed_profile == 'auto' else args.timed_profile == 'on'
+    # (season too: its profiled second pass would repeat the whole timed run)
+    tprof = (args.workload in ('day', 'days', 'season')) if args.timed_profile == 'auto' else args.timed_profile == 'on'
     sess = None if single else _lib.Session(device=gpu, device_inputs=True, profile=tprof, max_pool=args.max_pool)
     if single:  # config 1: blocking one-shot calls (per-cell latency)
         for item in dev_warm:
