@@ -175,6 +175,113 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
   }
 }
 
+// ------------------------------------------------------------------ k_gemm128
+// The same product on 128 x 128 output tiles, 512 threads (wave w: rows
+// 32 (w >> 1) .., columns 64 (w & 1) .. as 2 x 4 MFMA blocks, the gemm4 core
+// of oi_gemm.h): a streamed 16-deep chunk feeds twice the outputs of k_gemm's,
+// half the operand traffic per flop.  Every output is accumulated by the same
+// MFMA sequence over k as in k_gemm (chunks of 16, MFMA k-steps of 4 in
+// order), so the two kernels are bitwise equal and the wrapper may pick either
+// by shape.  tri == 0 only.  LDS: two (A, B) buffers of 16 x 128 chunks, row
+// stride 144 (rows k, k+1 in opposite bank halves); the epilogue stages the
+// tile 64 columns at a time.
+#define GT2 128
+#define GLD2 144
+template <bool TA, bool TB>
+__global__ __launch_bounds__(512) void k_gemm128(const Gemm* __restrict__ gs) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GKC * GLD2];
+  const Gemm g = gs[blockIdx.y];
+  const int tm = (g.m + GT2 - 1) / GT2, tn = (g.n + GT2 - 1) / GT2;
+  if ((int)blockIdx.x >= tm * tn) return;
+  const int it = blockIdx.x % tm, jt = blockIdx.x / tm;
+  const int kmax = g.k;
+  const int m0 = GT2 * it, n0 = GT2 * jt;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  Quad8 acc;
+  quad8_zero(acc);
+  const int nch = (kmax + GKC - 1) / GKC;
+  double ra[4], rb[4];
+  const Rsrc rA = rsrc(g.A), rB = rsrc(g.B);
+  // element e = t + 512 q of a 128 x 16 chunk: A(m, k) and op(B)(k, n)
+  auto load = [&](int ch) __attribute__((always_inline)) {
+    const int k0 = ch * GKC;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 512 * q;
+      int m, k;
+      if (TA) { k = e & 15; m = e >> 4; } else { m = e & 127; k = e >> 7; }
+      const int gm = m0 + m, gk = k0 + k;
+      ra[q] = bload(rA, gm < g.m && gk < kmax, TA ? gk + (size_t)g.lda * gm : gm + (size_t)g.lda * gk);
+      int n, kb;
+      if (TB) { n = e & 127; kb = e >> 7; } else { kb = e & 15; n = e >> 4; }
+      const int gn = n0 + n, gkb = k0 + kb;
+      rb[q] = bload(rB, gn < g.n && gkb < kmax, TB ? gn + (size_t)g.ldb * gkb : gkb + (size_t)g.ldb * gn);
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    double* As = lds + buf * 2 * GKC * GLD2;
+    double* Bs = As + GKC * GLD2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 512 * q;
+      if (TA) As[(e & 15) * GLD2 + (e >> 4)] = ra[q]; else As[(e >> 7) * GLD2 + (e & 127)] = ra[q];
+      if (TB) Bs[(e >> 7) * GLD2 + (e & 127)] = rb[q]; else Bs[(e & 15) * GLD2 + (e >> 4)] = rb[q];
+    }
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const double* As = lds + buf * 2 * GKC * GLD2;
+    const double* Bs = As + GKC * GLD2;
+#pragma unroll
+    for (int kk = 0; kk < GKC / 4; ++kk) {
+      const int k = kk * 4 + fk;
+      const double a0 = As[k * GLD2 + 32 * wr + fr], a1 = As[k * GLD2 + 32 * wr + 16 + fr];
+      double b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[q] = Bs[k * GLD2 + 64 * wc + 16 * q + fr];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc.c[0][q] = MFMA64(a0, b[q], acc.c[0][q]);
+        acc.c[1][q] = MFMA64(a1, b[q], acc.c[1][q]);
+      }
+    }
+  };
+  if (nch > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      if (ch + 1 < nch) load(ch + 1);
+      compute(ch & 1);
+      if (ch + 1 < nch) store((ch + 1) & 1);
+      __syncthreads();
+    }
+  }
+  // stage 64 columns at a time column-major in LDS (X[n * 129 + m]) for
+  // coalesced stores; waves with wc == h own columns 64 h .. 64 h + 63
+  double* X = lds;
+  for (int h = 0; h < 2; ++h) {
+    if (wc == h) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) X[(acc4_col(nb) - 64 * h) * 129 + acc4_row(mb, r)] = acc.c[mb][nb][r];
+    }
+    __syncthreads();
+    for (int e = t; e < GT2 * 64; e += 512) {
+      const int m = e & 127, n = e >> 7, gm = m0 + m, gn = n0 + 64 * h + n;
+      if (gm < g.m && gn < g.n) {
+        gdouble* c = G(g.C) + gm + (size_t)g.ldc * gn;
+        const double v = g.alpha * X[n * 129 + m];
+        *c = g.beta == 0.0 ? v : v + g.beta * *c;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ k_gemv
 // trans: y_j = alpha sum_i A(i, j) x_i + beta y_j, one wave per output;
 // else  y_i = alpha sum_j A(i, j) x_j + beta y_i, one thread per output.
@@ -1069,9 +1176,17 @@ static void check_extent(int64_t ld, int64_t rows, int64_t cols, const char* wha
     throw LinalgErr{std::string(what) + ": operand extent >= 2 GiB (32-bit buffer offsets)"};
 }
 
+// OI_GEMM128=0 keeps every product on the 64 x 64 kernel (A/B switch, read
+// per call so a test can flip it)
+static bool gemm128_ok() {
+  const char* e = std::getenv("OI_GEMM128");
+  return !(e && e[0] == '0');
+}
+
 void gemm(Stager& S, hipStream_t st, bool ta, bool tb, const std::vector<Gemm>& g) {
   std::vector<Gemm> live;
-  int tiles = 0;
+  int tiles = 0, tiles2 = 0;
+  bool wide = gemm128_ok();
   for (const Gemm& x : g) {
     if (x.m > 0 && x.n > 0 && x.k > 0) {
       check_extent(x.lda, ta ? x.k : x.m, ta ? x.m : x.k, "gemm A");
@@ -1081,10 +1196,21 @@ void gemm(Stager& S, hipStream_t st, bool ta, bool tb, const std::vector<Gemm>& 
     if (x.m > 0 && x.n > 0) {
       live.push_back(x);
       tiles = std::max(tiles, ((x.m + GT - 1) / GT) * ((x.n + GT - 1) / GT));
+      tiles2 = std::max(tiles2, ((x.m + GT2 - 1) / GT2) * ((x.n + GT2 - 1) / GT2));
+      wide = wide && x.tri == 0 && x.m >= GT2 && x.n >= GT2 && x.k >= 4 * GKC;
     }
   }
   if (live.empty()) return;
   const Gemm* dg = S.put(live);
+  if (wide) {  // bitwise equal to k_gemm (see k_gemm128)
+    dim3 grid2((unsigned)tiles2, (unsigned)live.size());
+    if (ta && tb) hipLaunchKernelGGL((k_gemm128<true, true>), grid2, dim3(512), 0, st, dg);
+    else if (ta) hipLaunchKernelGGL((k_gemm128<true, false>), grid2, dim3(512), 0, st, dg);
+    else if (tb) hipLaunchKernelGGL((k_gemm128<false, true>), grid2, dim3(512), 0, st, dg);
+    else hipLaunchKernelGGL((k_gemm128<false, false>), grid2, dim3(512), 0, st, dg);
+    LC(hipGetLastError());
+    return;
+  }
   dim3 grid((unsigned)tiles, (unsigned)live.size());
   if (ta && tb) hipLaunchKernelGGL((k_gemm<true, true>), grid, dim3(256), 0, st, dg);
   else if (ta) hipLaunchKernelGGL((k_gemm<true, false>), grid, dim3(256), 0, st, dg);
