@@ -1344,28 +1344,44 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   hipLaunchKernelGGL(k_stein_out, dim3(n, nto * nto), dim3(256), 0, st, de);
   LC(hipGetLastError());
   phase(2);
-  // BCGS2 over panels of TNB eigenvectors (columns of Z = E.A)
-  for (int p = 0; p < Mmax; p += TNB) {
-    if (p > 0) {
-      for (int pass = 0; pass < 2; ++pass) {
-        std::vector<Gemm> h, u;
-        for (const Eigh& e : es) {
-          if (e.M <= p) continue;
-          EighWs w = carve(e.work, e.M);
-          const int nb = std::min(TNB, e.M - p);
-          // H = Z(:, :p)' Z(:, p:p+nb)   (p x nb, ld M)
-          h.push_back(Gemm{e.A, e.A + (size_t)e.lda * p, w.H, p, nb, e.M, e.lda, e.lda, e.M, 1.0, 0.0, 0});
-          // Z(:, p:p+nb) -= Z(:, :p) H
-          u.push_back(Gemm{e.A, w.H, e.A + (size_t)e.lda * p, e.M, nb, p, e.lda, e.M, e.lda, -1.0, 1.0, 0});
-        }
-        gemm(S, st, true, false, h);
-        gemm(S, st, false, false, u);
+  // BCGS2 over blocks of `ob` eigenvectors (columns of Z = E.A): a block is
+  // projected out of every earlier block twice (two wide products per pass,
+  // k_gemm128 where the shapes allow), then orthogonalised inside as BCGS2
+  // over its TNB-column panels (k_orth_panel / k_mgs_panel).  ob = TNB is
+  // plain panel-wise BCGS2 (rounds 4-5); wider blocks do the same projections
+  // in a quarter of the launches on full 128-column tiles.  H lives in stein's
+  // scratch (free once k_stein_out has written Z).
+  static const int ob = [] {
+    const char* e = getenv("OI_ORTH_BLOCK");
+    const int v = e ? atoi(e) : 4 * TNB;
+    return v <= TNB ? TNB : v >= 8 * TNB ? 8 * TNB : (v / TNB) * TNB;
+  }();
+  auto project = [&](int lo, int p, int nbmax) {  // Z(:, p:p+nb) -= Z(:, lo:p) Z(:, lo:p)' Z(:, p:p+nb), twice
+    for (int pass = 0; pass < 2; ++pass) {
+      std::vector<Gemm> h, u;
+      for (const Eigh& e : es) {
+        if (e.M <= p) continue;
+        EighWs w = carve(e.work, e.M);
+        const int nb = std::min(nbmax, e.M - p), k = p - lo;
+        const double* Zlo = e.A + (size_t)e.lda * lo;
+        // H = Z(:, lo:p)' Z(:, p:p+nb)   (k x nb, ld M)
+        h.push_back(Gemm{Zlo, e.A + (size_t)e.lda * p, w.scr, k, nb, e.M, e.lda, e.lda, e.M, 1.0, 0.0, 0});
+        // Z(:, p:p+nb) -= Z(:, lo:p) H
+        u.push_back(Gemm{Zlo, w.scr, e.A + (size_t)e.lda * p, e.M, nb, k, e.lda, e.M, e.lda, -1.0, 1.0, 0});
       }
+      gemm(S, st, true, false, h);
+      gemm(S, st, false, false, u);
     }
-    hipLaunchKernelGGL(k_orth_panel, dim3(n), dim3(MG_T), 0, st, de, p);
-    LC(hipGetLastError());
-    hipLaunchKernelGGL(k_mgs_panel, dim3(n), dim3(MG_T), 0, st, de, p);
-    LC(hipGetLastError());
+  };
+  for (int P = 0; P < Mmax; P += ob) {
+    if (P > 0) project(0, P, ob);
+    for (int p = P; p < std::min(P + ob, Mmax); p += TNB) {
+      if (p > P) project(P, p, TNB);
+      hipLaunchKernelGGL(k_orth_panel, dim3(n), dim3(MG_T), 0, st, de, p);
+      LC(hipGetLastError());
+      hipLaunchKernelGGL(k_mgs_panel, dim3(n), dim3(MG_T), 0, st, de, p);
+      LC(hipGetLastError());
+    }
   }
   // back-transform: Z <- (I - V_p T_p V_p') Z for the panels in reverse order
   phase(3);

@@ -2,6 +2,7 @@
 // variant's M = 925 padded to 928, 32 per chunk) (build: tools/build_eigh_probe.sh).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -73,5 +74,23 @@ int main(int argc, char** argv) {
   std::vector<double> wh((size_t)M * nb);
   CK(hipMemcpy(wh.data(), w, wh.size() * 8, hipMemcpyDeviceToHost));
   printf("eigenvalues of matrix 0: min %.3e max %.3e\n", wh[0], wh[M - 1]);
+  // matrix 0's eigenvectors: orthogonality max |U'U - I| and residual max |AU - U diag(w)| / max|A|
+  std::vector<double> Uh(MM);
+  CK(hipMemcpy(Uh.data(), A, MM * 8, hipMemcpyDeviceToHost));
+  double orth = 0.0, res = 0.0, amax = 0.0;
+  for (size_t i = 0; i < MM; ++i) amax = std::max(amax, std::fabs(h[i]));
+  for (int a = 0; a < M; ++a)
+    for (int b = 0; b <= a; ++b) {
+      double s = 0.0;
+      for (int i = 0; i < M; ++i) s += Uh[i + (size_t)M * a] * Uh[i + (size_t)M * b];
+      orth = std::max(orth, std::fabs(s - (a == b ? 1.0 : 0.0)));
+    }
+  for (int b = 0; b < M; ++b)
+    for (int i = 0; i < M; ++i) {
+      double s = 0.0;
+      for (int k = 0; k < M; ++k) s += h[i + (size_t)M * k] * Uh[k + (size_t)M * b];
+      res = std::max(res, std::fabs(s - wh[b] * Uh[i + (size_t)M * b]));
+    }
+  printf("matrix 0: orthogonality %.3e, residual %.3e x max|A|\n", orth, res / amax);
   return 0;
 }
