@@ -13,11 +13,12 @@
 //   k_potrf_tile  Cholesky + inverse of one 64 x 64 diagonal block per matrix
 //                 (the blocked right-looking factorisation: potrf_tile ->
 //                 panel product with the block inverse -> lower-tile update)
-//   k_sy_reflect / k_sy_symv / k_sy_w
+//   k_sy_symv / k_sy_w
 //                 Householder tridiagonalisation (LAPACK dsytrd / dlatrd,
-//                 lower), three launches per column over the batch: the
-//                 column's reflector, the symmetric product over the trailing
-//                 lower triangle on OI_SY_S workgroups per matrix, the w vector;
+//                 lower), two launches per column over the batch: the
+//                 column's reflector and the symmetric product over the
+//                 trailing lower triangle on OI_SY_S workgroups per matrix,
+//                 then the w vector and the next column's update by rows;
 //                 per 32-column panel the rank-64 trailing update on k_gemm;
 //                 V (unit lower, clean copy) and T (dlarft, forward
 //                 columnwise) kept per panel
@@ -418,104 +419,82 @@ __device__ __forceinline__ void wg_sum(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
-// dynamic LDS: yw[SY_W][M] | v[M] | red[64]
 __device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] = E.A[0]; }
 
-// The tridiagonalisation runs column by column as three launches per column
+// The tridiagonalisation runs column by column as two launches per column
 // g = p + i (panel p, i < 32) over the whole batch -- the symmetric product
 // y = A22 v streams the trailing lower triangle once per column, and one
 // workgroup per matrix could pull it only at ~40 GB/s (a CU's outstanding
-// misses bound it; measured round 4), so it is spread over ns workgroups
-// per matrix:
-//   k_sy_reflect(p, i)  column g brought up to date with the panel's earlier
-//                       reflectors, the reflector v_g (dlarfg): d, e, tau, V
-//   k_sy_symv(p, i)     partial y of ns workgroups (their waves own groups of
-//                       SY_C consecutive columns) and the panel dots V'v, W'v
-//   k_sy_w(p, i)        y summed in a fixed order, w = tau (y - V(W'v) - W(V'v))
-//                       - tau/2 (w'v) v, column i of the panel's T (dlarft)
+// misses bound it; measured round 4), so it is spread over ns workgroups per
+// matrix, and so is everything else that streams the panel:
+//   k_sy_symv(p, i)  every workgroup forms the reflector v_g of column g
+//                    (dlarfg; identical fixed-order reductions, workgroup 0
+//                    publishes v, d, e, tau), then its partial y (its waves
+//                    own groups of SY_C consecutive columns), its share of the
+//                    panel dots V'v, W'v and its partial y'v
+//   k_sy_w(p, i)     SW_T rows per workgroup: w = tau (y - V(W'v) - W(V'v))
+//                    - tau/2 (w'v) v with w'v = tau (y'v - 2 (W'v).(V'v)) from
+//                    the dots, column i of the panel's T (dlarft, forward
+//                    columnwise), and column g + 1 brought up to date with the
+//                    panel's reflectors 0 .. i (dlatrd's column update)
 // then, per panel, the trailing update A22 -= V W' + W V' on oila::gemm.
 // symv workgroups per matrix: gridDim.y of k_sy_symv (OI_SY_S, default below)
 #define SY_S_DEFAULT 8
 #define SY_S_MAX TNB  // the partials live in the M x 32 H block
-// column g = p + i: brought up to date with the panel's earlier reflectors,
-// then its reflector (the body of k_sy_reflect; k_sy_w(i) also runs it for
-// column i + 1, which saves one launch per column)
-__device__ __forceinline__ void sy_reflect(const Eigh& E, int p, int i, double* red) {
-  const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i;
-  if (p >= M - 1) {
-    if (p == 0 && i == 0 && t == 0) ws_d0(E);  // M == 1
-    return;
-  }
-  if (g >= M - 1) return;  // this matrix's last panel is shorter
-  gdouble* A = G(E.A);
-  EighWsG ws = carveG(E.work, M);
-  const Rsrc rV = rsrc(carve(E.work, M).Vc + (size_t)M * p), rW = rsrc(carve(E.work, M).Ws);  // panel V, W
-  // (1) A(r,g) -= V(r,q) W(g,q) + W(r,q) V(g,q), q < i; two rows per thread
-  if (i > 0) {
-    for (int ra = g + t; ra < M; ra += 2 * SY_T) {
-      const int rb = ra + SY_T;
-      const bool okb = rb < M;
-      double sa = A[ra + (size_t)ld * g], sb = okb ? A[rb + (size_t)ld * g] : 0.0;
-#pragma unroll 8
-      for (int q = 0; q < i; ++q) {
-        const double wg = ws.Ws[(size_t)M * q + g], vg = ws.Vc[(size_t)M * (p + q) + g];
-        const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
-        const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
-        sa -= va * wg + wa * vg;
-        sb -= vb * wg + wb * vg;
-      }
-      A[ra + (size_t)ld * g] = sa;
-      if (okb) A[rb + (size_t)ld * g] = sb;
-    }
-    __syncthreads();
-  }
-  // (2) reflector annihilating A(g+2:M, g) (dlarfg)
-  double xs[1] = {0.0};
-  for (int r = g + 2 + t; r < M; r += SY_T) {
-    const double a = A[r + (size_t)ld * g];
-    xs[0] += a * a;
-  }
-  wg_sum<1>(xs, red);
-  const double alpha = A[g + 1 + (size_t)ld * g];
-  const double xn = sqrt(xs[0]);
-  double tau, beta, scal;
-  if (xn == 0.0) {
-    tau = 0.0;
-    beta = alpha;
-    scal = 0.0;
-  } else {
-    beta = -copysign(sqrt(alpha * alpha + xn * xn), alpha);
-    tau = (beta - alpha) / beta;
-    scal = 1.0 / (alpha - beta);
-  }
-  gdouble* vg = ws.Vc + (size_t)M * g;
-  for (int r = t; r < M; r += SY_T) vg[r] = r < g + 1 ? 0.0 : r == g + 1 ? 1.0 : A[r + (size_t)ld * g] * scal;
-  if (t == 0) {
-    ws.d[g] = A[g + (size_t)ld * g];
-    ws.e[g] = beta;
-    ws.tau[g] = tau;
-  }
-}
-
-__global__ __launch_bounds__(SY_T) void k_sy_reflect(const Eigh* __restrict__ es, int p, int i) {
-  __shared__ double red[64];
-  const Eigh E = es[blockIdx.x];
-  sy_reflect(E, p, i, red);
-}
+#define SW_T 128      // k_sy_w: rows (threads) per workgroup
 
 // partial y of workgroup s into H[s M + r] (rows g+1 .. M-1); the panel dots
-// pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g) into X[0 .. 2 TNB)
+// pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g) into X[0 .. 2 TNB);
+// the partial y'v into X[2 TNB + s].  dynamic LDS: yw[SY_W][M] | v[M] | red[64]
 __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, int p, int i) {
   extern __shared__ double sm[];
   const Eigh E = es[blockIdx.x];
   const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63, g = p + i, sgrp = blockIdx.y;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // provably wave-uniform (buffer descriptors)
-  if (g >= M - 1) return;
+  if (p >= M - 1) {
+    if (p == 0 && i == 0 && t == 0 && sgrp == 0) ws_d0(E);  // M == 1
+    return;
+  }
+  if (g >= M - 1) return;  // this matrix's last panel is shorter
   EighWsG ws = carveG(E.work, M);
   double* yw = sm;
   double* v = yw + (size_t)SY_W * M;
+  double* red = v + M;
+  // (2) the reflector annihilating A(g+2:M, g) (dlarfg); column g is up to
+  // date (k_sy_w(i - 1), or the trailing update for i = 0)
+  const gdouble* A = G(E.A);
+  {
+    double xs[1] = {0.0};
+    for (int r = g + 2 + t; r < M; r += SY_T) {
+      const double a = A[r + (size_t)ld * g];
+      xs[0] += a * a;
+    }
+    wg_sum<1>(xs, red);
+    const double alpha = A[g + 1 + (size_t)ld * g];
+    const double xn = sqrt(xs[0]);
+    double tau, beta, scal;
+    if (xn == 0.0) {
+      tau = 0.0;
+      beta = alpha;
+      scal = 0.0;
+    } else {
+      beta = -copysign(sqrt(alpha * alpha + xn * xn), alpha);
+      tau = (beta - alpha) / beta;
+      scal = 1.0 / (alpha - beta);
+    }
+    gdouble* vg = ws.Vc + (size_t)M * g;
+    for (int r = t; r < M; r += SY_T) {
+      const double x = r < g + 1 ? 0.0 : r == g + 1 ? 1.0 : A[r + (size_t)ld * g] * scal;
+      v[r] = x;
+      if (sgrp == 0) vg[r] = x;
+    }
+    if (sgrp == 0 && t == 0) {
+      ws.d[g] = A[g + (size_t)ld * g];
+      ws.e[g] = beta;
+      ws.tau[g] = tau;
+    }
+  }
   for (int r = t; r < SY_W * M; r += SY_T) yw[r] = 0.0;
-  for (int r = t; r < M; r += SY_T) v[r] = ws.Vc[(size_t)M * g + r];
   __syncthreads();
   // (3) y = A22 v over the lower triangle of A(g+1:M, g+1:M): global wave
   // gw = s SY_W + wv owns the groups of SY_C consecutive columns
@@ -585,88 +564,95 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
   }
   __syncthreads();
   gdouble* yp = ws.H + (size_t)sgrp * M;
+  double yv[1] = {0.0};
   for (int r = g + 1 + t; r < M; r += SY_T) {
     double sy = 0.0;
 #pragma unroll
     for (int ww = 0; ww < SY_W; ++ww) sy += yw[(size_t)ww * M + r];
     yp[r] = sy;
+    yv[0] += sy * v[r];
   }
+  wg_sum<1>(yv, red);
+  if (t == 0) ws.X[2 * TNB + sgrp] = yv[0];
 }
 
-__global__ __launch_bounds__(SY_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i, int ns, int next) {
-  __shared__ double red[64];
+// grid (matrices, ceil(Mmax / SW_T)): thread t of workgroup b owns row
+// g + 1 + SW_T b + t
+__global__ __launch_bounds__(SW_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i, int ns, int next) {
   __shared__ double pan[2 * TNB];
+  __shared__ double rowg1[2 * TNB + 1];  // W(g+1, q), V(g+1, q) for q <= i; w_i(g+1)
   const Eigh E = es[blockIdx.x];
-  const int M = E.M, t = threadIdx.x, g = p + i;
+  const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i;
   if (g >= M - 1) return;
+  const int r = g + 1 + SW_T * blockIdx.y + t;
+  if (g + 1 + SW_T * blockIdx.y >= M) return;  // no rows for this workgroup (uniform)
   EighWsG ws = carveG(E.work, M);
   const Rsrc rV = rsrc(carve(E.work, M).Vc + (size_t)M * p), rW = rsrc(carve(E.work, M).Ws);
   const double tau = ws.tau[g];
   if (t < 2 * TNB) pan[t] = t % TNB < i ? ws.X[t] : 0.0;
-  // column i of the block reflector's T (dlarft, forward columnwise), in the
-  // workspace: T(i,i) = tau, T(a,i) = -tau sum_{a<=k<i} T(a,k) (V_k'v)
-  gdouble* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
-  if (i == 0)
-    for (int e = t; e < TNB * TNB; e += SY_T) Tp[e] = 0.0;
   __syncthreads();
-  if (t <= i) {
-    double x = tau;
-    if (t < i) {
-      x = 0.0;
-      for (int k = t; k < i; ++k) x += Tp[t + TNB * k] * pan[TNB + k];
-      x *= -tau;
-    }
-    Tp[t + TNB * i] = x;
-  }
-  // (4) w = tau (y - V (W'v) - W (V'v)), y = sum of the ns partials; then
-  // w += -tau/2 (w'v) v; two rows per thread
+  // w'v = tau (y'v - 2 (W'v).(V'v)), fixed order
+  double yv = 0.0, dd = 0.0;
+  for (int s = 0; s < ns; ++s) yv += ws.X[2 * TNB + s];
+  for (int q = 0; q < i; ++q) dd += pan[q] * pan[TNB + q];
+  const double a2 = -0.5 * tau * (tau * (yv - 2.0 * dd));
   const gdouble* vgc = ws.Vc + (size_t)M * g;
-  double sv[1] = {0.0};
-  double wr2[2][4];  // rows ra, rb of each sweep (M <= 4096: at most 4 sweeps)
-  int nsw = 0;
-  for (int ra = g + 1 + t; ra < M; ra += 2 * SY_T, ++nsw) {
-    const int rb = ra + SY_T;
-    const bool okb = rb < M;
-    double sa = 0.0, sb = 0.0;
-#pragma unroll
-    for (int s = 0; s < ns; ++s) {
-      sa += ws.H[(size_t)s * M + ra];
-      if (okb) sb += ws.H[(size_t)s * M + rb];
-    }
+  // w_i(row) = tau (y - V(row,:) W'v - W(row,:) V'v) + a2 v(row)
+  auto wrow = [&](int rr) {
+    double sa = 0.0;
+    for (int s = 0; s < ns; ++s) sa += ws.H[(size_t)s * M + rr];
 #pragma unroll 8
     for (int q = 0; q < i; ++q) {
-      const double va = bload(rV, true, (size_t)M * q + ra), wa = bload(rW, true, (size_t)M * q + ra);
-      const double vb = bload(rV, okb, (size_t)M * q + rb), wb = bload(rW, okb, (size_t)M * q + rb);
+      const double va = bload(rV, true, (size_t)M * q + rr), wa = bload(rW, true, (size_t)M * q + rr);
       sa -= va * pan[q] + wa * pan[TNB + q];
-      sb -= vb * pan[q] + wb * pan[TNB + q];
     }
-    const double wra = tau * sa;
-    sv[0] += wra * vgc[ra];
-    double wrb = 0.0;
-    if (okb) {
-      wrb = tau * sb;
-      sv[0] += wrb * vgc[rb];
-    }
-    if (nsw < 4) {
-      wr2[0][nsw] = wra;
-      wr2[1][nsw] = wrb;
-    }
-  }
-  wg_sum<1>(sv, red);
-  const double a2 = -0.5 * tau * sv[0];
+    return tau * sa + a2 * vgc[rr];
+  };
   gdouble* wcol = ws.Ws + (size_t)M * i;
-  for (int r = t; r <= g && r < M; r += SY_T) wcol[r] = 0.0;
-  nsw = 0;
-  for (int ra = g + 1 + t; ra < M; ra += 2 * SY_T, ++nsw) {
-    const int rb = ra + SY_T;
-    if (nsw < 4) {
-      wcol[ra] = wr2[0][nsw] + a2 * vgc[ra];
-      if (rb < M) wcol[rb] = wr2[1][nsw] + a2 * vgc[rb];
-    }
-  }
-  if (next) {  // the panel's next column (w column i is visible to the workgroup)
+  if (blockIdx.y == 0) {
+    // column i of the block reflector's T (dlarft, forward columnwise), in the
+    // workspace: T(i,i) = tau, T(a,i) = -tau sum_{a<=k<i} T(a,k) (V_k'v)
+    gdouble* Tp = ws.T + (size_t)(p / TNB) * TNB * TNB;
+    if (i == 0)
+      for (int e = t; e < TNB * TNB; e += SW_T) Tp[e] = 0.0;
     __syncthreads();
-    sy_reflect(E, p, i + 1, red);
+    if (t <= i) {
+      double x = tau;
+      if (t < i) {
+        x = 0.0;
+        for (int k = t; k < i; ++k) x += Tp[t + TNB * k] * pan[TNB + k];
+        x *= -tau;
+      }
+      Tp[t + TNB * i] = x;
+    }
+    for (int rr = t; rr <= g && rr < M; rr += SW_T) wcol[rr] = 0.0;
+  }
+  double w = 0.0;
+  if (r < M) {
+    w = wrow(r);
+    wcol[r] = w;
+  }
+  if (!next || g + 1 >= M - 1) return;
+  // column g1 = g + 1, rows >= g1: A(r,g1) -= V(r,q) W(g1,q) + W(r,q) V(g1,q), q <= i
+  const int g1 = g + 1;
+  if (t <= i) {
+    rowg1[t] = t < i ? ws.Ws[(size_t)M * t + g1] : 0.0;
+    rowg1[TNB + t] = ws.Vc[(size_t)M * (p + t) + g1];
+  }
+  if (t == 0) rowg1[2 * TNB] = wrow(g1);
+  __syncthreads();
+  if (t == 0) rowg1[i] = rowg1[2 * TNB];
+  __syncthreads();
+  if (r < M) {
+    gdouble* A = G(E.A);
+    double sa = A[r + (size_t)ld * g1];
+#pragma unroll 8
+    for (int q = 0; q < i; ++q) {
+      const double va = bload(rV, true, (size_t)M * q + r), wa = bload(rW, true, (size_t)M * q + r);
+      sa -= va * rowg1[q] + wa * rowg1[TNB + q];
+    }
+    sa -= vgc[r] * rowg1[i] + w * rowg1[TNB + i];
+    A[r + (size_t)ld * g1] = sa;
   }
 }
 
@@ -1298,7 +1284,8 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   if (Mmax > 4096) throw LinalgErr{"eigh: M > 4096 not supported"};
   const Eigh* de = S.put(es);
   const unsigned n = (unsigned)es.size();
-  const size_t lds_sy = (size_t)(SY_W + 1) * Mmax * sizeof(double);
+  const size_t lds_sy = ((size_t)(SY_W + 1) * Mmax + 64) * sizeof(double);
+  const unsigned nsw = (unsigned)((Mmax + SW_T - 1) / SW_T);
   if (lds_sy > 160 * 1024) throw LinalgErr{"eigh: matrix too large for the tridiagonalisation's LDS"};
   static const int ns = [] {
     const char* e = getenv("OI_SY_S");
@@ -1311,11 +1298,10 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   // batched GEMMs over the whole chip
   for (int p = 0; p < std::max(Mmax - 1, 1); p += TNB) {
     for (int i = 0; i < TNB && (i == 0 || p + i < Mmax - 1); ++i) {
-      // the panel's first reflector has a launch of its own; k_sy_w(i) forms the next
-      if (i == 0) hipLaunchKernelGGL(k_sy_reflect, dim3(n), dim3(SY_T), 0, st, de, p, i);
+      // k_sy_symv forms column g's reflector; k_sy_w(i) brings column g + 1 up to date
       hipLaunchKernelGGL(k_sy_symv, dim3(n, ns), dim3(SY_T), lds_sy, st, de, p, i);
       const int next = i + 1 < TNB && p + i + 1 < Mmax - 1;
-      hipLaunchKernelGGL(k_sy_w, dim3(n), dim3(SY_T), 0, st, de, p, i, ns, next);
+      hipLaunchKernelGGL(k_sy_w, dim3(n, nsw), dim3(SW_T), 0, st, de, p, i, ns, next);
     }
     LC(hipGetLastError());
     std::vector<Gemm> g1, g2;
