@@ -365,7 +365,7 @@ __global__ __launch_bounds__(64) void k_potrf_tile(const Chol* __restrict__ cs, 
 #define SY_T 512 // threads
 #define SY_W (SY_T / 64)
 #define SY_C 8   // symv: columns per wave group
-#define SY_R 8   // symv: 64-row chunks per load batch
+#define SY_R 4   // symv: 64-row chunks per load batch (8: 190 VGPRs, one workgroup per CU)
 
 struct EighWs {  // per-matrix workspace carve-up (eigh_workspace_doubles)
   double *Vc, *Ws, *T, *d, *e, *tau, *scr, *H, *X, *Y, *flag;
@@ -446,7 +446,8 @@ __device__ __forceinline__ void ws_d0(const Eigh& E) { carve(E.work, E.M).d[0] =
 // partial y of workgroup s into H[s M + r] (rows g+1 .. M-1); the panel dots
 // pan[q] = W(:,q)'v, pan[TNB + q] = V(:,q)'v (rows > g) into X[0 .. 2 TNB);
 // the partial y'v into X[2 TNB + s].  dynamic LDS: yw[SY_W][M] | v[M] | red[64]
-__global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, int p, int i) {
+// at most 128 VGPRs: two 512-thread workgroups per CU (their LDS fits too)
+__global__ __launch_bounds__(SY_T) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sy_symv(const Eigh* __restrict__ es, int p, int i) {
   extern __shared__ double sm[];
   const Eigh E = es[blockIdx.x];
   const int M = E.M, ld = E.lda, t = threadIdx.x, lane = t & 63, g = p + i, sgrp = blockIdx.y;
@@ -497,15 +498,20 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
   for (int r = t; r < SY_W * M; r += SY_T) yw[r] = 0.0;
   __syncthreads();
   // (3) y = A22 v over the lower triangle of A(g+1:M, g+1:M): global wave
-  // gw = s SY_W + wv owns the groups of SY_C consecutive columns
-  // c0 = g+1 + SY_C (gw + SY_S SY_W j) and streams their rows in batches of
+  // gw = s SY_W + wv owns groups of SY_C consecutive columns (dealt below)
+  // and streams their rows in batches of
   // SY_R x 64; per row one v[r] read and one yw[wv][r] read-modify-write (the
   // transposed half) serve the whole group; the group's column dots are
   // reduced once at its end
   double* myw = yw + (size_t)wv * M;
   const int gw = sgrp * SY_W + wv;
-  const int ns = gridDim.y;
-  for (int c0 = g + 1 + SY_C * gw; c0 < M; c0 += SY_C * SY_W * ns) {
+  const int ns = gridDim.y, nw = SY_W * ns;
+  // groups dealt in snake order (k = j nw + gw, then j nw + nw - 1 - gw, ...):
+  // a wave's long early group pairs with a short late one (round-robin left
+  // the first waves ~1.6x the mean rows)
+  for (int jg = 0;; ++jg) {
+    const int c0 = g + 1 + SY_C * (jg * nw + ((jg & 1) ? nw - 1 - gw : gw));
+    if (c0 >= M) break;
     const Rsrc rcol = rsrc(E.A + (size_t)ld * c0);
     double vc[SY_C], dot[SY_C];
 #pragma unroll
@@ -580,7 +586,7 @@ __global__ __launch_bounds__(SY_T) void k_sy_symv(const Eigh* __restrict__ es, i
 // g + 1 + SW_T b + t
 __global__ __launch_bounds__(SW_T) void k_sy_w(const Eigh* __restrict__ es, int p, int i, int ns, int next) {
   __shared__ double pan[2 * TNB];
-  __shared__ double rowg1[2 * TNB + 1];  // W(g+1, q), V(g+1, q) for q <= i; w_i(g+1)
+  __shared__ double rowg1[2 * TNB + 1];  // W(g+1, q), V(g+1, q) for q < i; w_i(g+1)
   const Eigh E = es[blockIdx.x];
   const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i;
   if (g >= M - 1) return;
@@ -601,9 +607,11 @@ __global__ __launch_bounds__(SW_T) void k_sy_w(const Eigh* __restrict__ es, int 
   auto wrow = [&](int rr) {
     double sa = 0.0;
     for (int s = 0; s < ns; ++s) sa += ws.H[(size_t)s * M + rr];
-#pragma unroll 8
-    for (int q = 0; q < i; ++q) {
-      const double va = bload(rV, true, (size_t)M * q + rr), wa = bload(rW, true, (size_t)M * q + rr);
+    // all TNB columns' loads in flight at once; q >= i loads 0 against pan = 0,
+    // and sa - (+0) == sa for every sa, so the sum is the q < i one exactly
+#pragma unroll
+    for (int q = 0; q < TNB; ++q) {
+      const double va = bload(rV, q < i, (size_t)M * q + rr), wa = bload(rW, q < i, (size_t)M * q + rr);
       sa -= va * pan[q] + wa * pan[TNB + q];
     }
     return tau * sa + a2 * vgc[rr];
@@ -635,23 +643,21 @@ __global__ __launch_bounds__(SW_T) void k_sy_w(const Eigh* __restrict__ es, int 
   if (!next || g + 1 >= M - 1) return;
   // column g1 = g + 1, rows >= g1: A(r,g1) -= V(r,q) W(g1,q) + W(r,q) V(g1,q), q <= i
   const int g1 = g + 1;
-  if (t <= i) {
+  if (t < TNB) {  // zeros from i on (the masked loop below adds exactly +0 there)
     rowg1[t] = t < i ? ws.Ws[(size_t)M * t + g1] : 0.0;
-    rowg1[TNB + t] = ws.Vc[(size_t)M * (p + t) + g1];
+    rowg1[TNB + t] = t < i ? ws.Vc[(size_t)M * (p + t) + g1] : 0.0;
   }
   if (t == 0) rowg1[2 * TNB] = wrow(g1);
-  __syncthreads();
-  if (t == 0) rowg1[i] = rowg1[2 * TNB];
   __syncthreads();
   if (r < M) {
     gdouble* A = G(E.A);
     double sa = A[r + (size_t)ld * g1];
-#pragma unroll 8
-    for (int q = 0; q < i; ++q) {
-      const double va = bload(rV, true, (size_t)M * q + r), wa = bload(rW, true, (size_t)M * q + r);
+#pragma unroll
+    for (int q = 0; q < TNB; ++q) {
+      const double va = bload(rV, q < i, (size_t)M * q + r), wa = bload(rW, q < i, (size_t)M * q + r);
       sa -= va * rowg1[q] + wa * rowg1[TNB + q];
     }
-    sa -= vgc[r] * rowg1[i] + w * rowg1[TNB + i];
+    sa -= vgc[r] * rowg1[2 * TNB] + w * vgc[g1];  // q = i: W(g1, i), V(g1, i) = v_g(g1)
     A[r + (size_t)ld * g1] = sa;
   }
 }

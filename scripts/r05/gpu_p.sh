@@ -1,0 +1,18 @@
+# round 5: symv column groups dealt in snake order: probe timings / accuracy,
+# kernel stats of the probe, Nystrom tests and line
+set -o pipefail
+export TMPDIR=/tmp
+D=gpurun_out/r05/p; mkdir -p $D
+timeout -k 10 180 tools/eigh_probe 928 64 > $D/eigh_probe.txt 2>&1 || { cat $D/eigh_probe.txt; exit 1; }
+echo "snake: $(tr '\n' ' ' < $D/eigh_probe.txt)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/trace -o run --output-format csv -- tools/eigh_probe 928 64 > $D/probe_prof.txt 2> $D/trace.err
+rc=$?; echo "rocprof rc $rc"; [ $rc -eq 0 ] || { tail -5 $D/trace.err; exit $rc; }
+find $D/trace -name "*kernel_stats.csv" -exec cp {} $D/kernel_stats.csv \;
+rm -rf $D/trace
+cut -c1-130 $D/kernel_stats.csv | head -12
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_nystrom.py -x -q --timeout 300 --timeout-method thread > $D/tests.log 2>&1
+rc=$?; tail -1 $D/tests.log; [ $rc -eq 0 ] || { tail -40 $D/tests.log; exit $rc; }
+timeout -k 10 400 python3 bench.py --workload nystrom --steps 10 --warmup 2 --no-cpu-baseline --out $D/nystrom.json > $D/nystrom.log 2>&1 || { tail -20 $D/nystrom.log; exit 1; }
+python3 -c "
+import json; d=json.load(open('$D/nystrom.json')); s=d['roofline']['stages_ms']
+print('snake', d['value'], {k: round(v) for k, v in sorted(s.items(), key=lambda x: -x[1])[:8]})"
