@@ -9,7 +9,7 @@
 //                 in 16-deep chunks, results staged through LDS for coalesced
 //                 column stores; one launch covers a batch of differently
 //                 sized products (grid.y = product)
-//   k_gemv        y = alpha op(A) x + beta y
+//   k_gemv_t/_n   y = alpha op(A) x + beta y
 //   k_potrf_tile  Cholesky + inverse of one 64 x 64 diagonal block per matrix
 //                 (the blocked right-looking factorisation: potrf_tile ->
 //                 panel product with the block inverse -> lower-tile update)
@@ -284,25 +284,40 @@ __global__ __launch_bounds__(512) void k_gemm128(const Gemm* __restrict__ gs) {
 }
 
 // ------------------------------------------------------------------ k_gemv
-// trans: y_j = alpha sum_i A(i, j) x_i + beta y_j, one wave per output;
-// else  y_i = alpha sum_j A(i, j) x_j + beta y_i, one thread per output.
-template <bool TRANS>
-__global__ __launch_bounds__(256) void k_gemv(const Gemv* __restrict__ gs) {
+// trans: y_j = alpha sum_i A(i, j) x_i + beta y_j, one wave per output.
+__global__ __launch_bounds__(256) void k_gemv_t(const Gemv* __restrict__ gs) {
   const Gemv g = gs[blockIdx.y];
-  if (TRANS) {
-    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (j >= g.n) return;
-    const double* a = g.A + (size_t)g.lda * j;
-    double s = 0.0;
-    for (int i = lane; i < g.m; i += 64) s += a[i] * g.x[i];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-    if (lane == 0) g.y[j] = g.beta == 0.0 ? g.alpha * s : g.alpha * s + g.beta * g.y[j];
-  } else {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= g.m) return;
-    double s = 0.0;
-    for (int j = 0; j < g.n; ++j) s += g.A[i + (size_t)g.lda * j] * g.x[j];
-    g.y[i] = g.beta == 0.0 ? g.alpha * s : g.alpha * s + g.beta * g.y[i];
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (j >= g.n) return;
+  const double* a = g.A + (size_t)g.lda * j;
+  double s = 0.0;
+  for (int i = lane; i < g.m; i += 64) s += a[i] * g.x[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if (lane == 0) g.y[j] = g.beta == 0.0 ? g.alpha * s : g.alpha * s + g.beta * g.y[j];
+}
+
+// else y_i = alpha sum_j A(i, j) x_j + beta y_i: 64 rows per workgroup (lane =
+// row, coalesced column reads), its GV_W waves take contiguous column ranges
+// and their partial sums are added in wave order (one thread per row over
+// all columns left the chip ~70 waves for an n x M = 4600 x 928 product)
+#define GV_W 16
+__global__ __launch_bounds__(64 * GV_W) void k_gemv_n(const Gemv* __restrict__ gs) {
+  __shared__ double part[GV_W][64];
+  const Gemv g = gs[blockIdx.y];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  if (blockIdx.x * 64 >= g.m) return;  // uniform
+  const int per = (g.n + GV_W - 1) / GV_W, j0 = w * per, j1 = min(g.n, j0 + per);
+  double s = 0.0;
+  if (i < g.m)
+#pragma unroll 8
+    for (int j = j0; j < j1; ++j) s += g.A[i + (size_t)g.lda * j] * g.x[j];
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i < g.m) {
+    double t = part[0][lane];
+    for (int ww = 1; ww < GV_W; ++ww) t += part[ww][lane];
+    g.y[i] = g.beta == 0.0 ? g.alpha * t : g.alpha * t + g.beta * g.y[i];
   }
 }
 
@@ -1223,9 +1238,9 @@ void gemv(Stager& S, hipStream_t st, bool trans, const std::vector<Gemv>& g) {
   if (live.empty()) return;
   const Gemv* dg = S.put(live);
   if (trans)
-    hipLaunchKernelGGL(k_gemv<true>, dim3((unsigned)((outs + 3) / 4), (unsigned)live.size()), dim3(256), 0, st, dg);
+    hipLaunchKernelGGL(k_gemv_t, dim3((unsigned)((outs + 3) / 4), (unsigned)live.size()), dim3(256), 0, st, dg);
   else
-    hipLaunchKernelGGL(k_gemv<false>, dim3((unsigned)((outs + 255) / 256), (unsigned)live.size()), dim3(256), 0,
+    hipLaunchKernelGGL(k_gemv_n, dim3((unsigned)((outs + 63) / 64), (unsigned)live.size()), dim3(64 * GV_W), 0,
                        st, dg);
   LC(hipGetLastError());
 }
