@@ -88,6 +88,11 @@ __device__ __forceinline__ double bload(Rsrc r, bool ok, size_t idx) {
 #define GT 64
 #define GKC 16
 #define GLD 80  // LDS row stride of a staged 16 x 64 chunk (rows k, k+1 in opposite bank halves)
+// A k-contiguous operand (A with TA, B without TB) is stored transposed: the
+// 16 lanes of a half-wave that hold one m and k = 0 .. 15 would hit two banks
+// (8-way conflicts), so element (k, m) sits at column m ^ (k >> 1) -- a
+// permutation inside m's aligned 8-block; the compute reads apply the same XOR
+// and stay conflict-free (k >> 1 is uniform across a half-wave's lanes).
 
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
@@ -129,8 +134,8 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = t + 256 * q;
-      if (TA) As[(e & 15) * GLD + (e >> 4)] = ra[q]; else As[(e >> 6) * GLD + (e & 63)] = ra[q];
-      if (TB) Bs[(e >> 6) * GLD + (e & 63)] = rb[q]; else Bs[(e & 15) * GLD + (e >> 4)] = rb[q];
+      if (TA) As[(e & 15) * GLD + ((e >> 4) ^ ((e & 15) >> 1))] = ra[q]; else As[(e >> 6) * GLD + (e & 63)] = ra[q];
+      if (TB) Bs[(e >> 6) * GLD + (e & 63)] = rb[q]; else Bs[(e & 15) * GLD + ((e >> 4) ^ ((e & 15) >> 1))] = rb[q];
     }
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
@@ -138,9 +143,9 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
     const double* Bs = As + GKC * GLD;
 #pragma unroll
     for (int kk = 0; kk < GKC / 4; ++kk) {
-      const int k = kk * 4 + fk;
-      const double a0 = As[k * GLD + 32 * wr + fr], a1 = As[k * GLD + 32 * wr + 16 + fr];
-      const double b0 = Bs[k * GLD + 32 * wc + fr], b1 = Bs[k * GLD + 32 * wc + 16 + fr];
+      const int k = kk * 4 + fk, sa = TA ? k >> 1 : 0, sb = TB ? 0 : k >> 1;
+      const double a0 = As[k * GLD + ((32 * wr + fr) ^ sa)], a1 = As[k * GLD + ((32 * wr + 16 + fr) ^ sa)];
+      const double b0 = Bs[k * GLD + ((32 * wc + fr) ^ sb)], b1 = Bs[k * GLD + ((32 * wc + 16 + fr) ^ sb)];
       acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
       acc.c[0][1] = MFMA64(a0, b1, acc.c[0][1]);
       acc.c[1][0] = MFMA64(a1, b0, acc.c[1][0]);
@@ -226,8 +231,8 @@ __global__ __launch_bounds__(512) void k_gemm128(const Gemm* __restrict__ gs) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = t + 512 * q;
-      if (TA) As[(e & 15) * GLD2 + (e >> 4)] = ra[q]; else As[(e >> 7) * GLD2 + (e & 127)] = ra[q];
-      if (TB) Bs[(e >> 7) * GLD2 + (e & 127)] = rb[q]; else Bs[(e & 15) * GLD2 + (e >> 4)] = rb[q];
+      if (TA) As[(e & 15) * GLD2 + ((e >> 4) ^ ((e & 15) >> 1))] = ra[q]; else As[(e >> 7) * GLD2 + (e & 127)] = ra[q];
+      if (TB) Bs[(e >> 7) * GLD2 + (e & 127)] = rb[q]; else Bs[(e & 15) * GLD2 + ((e >> 4) ^ ((e & 15) >> 1))] = rb[q];
     }
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
@@ -235,11 +240,11 @@ __global__ __launch_bounds__(512) void k_gemm128(const Gemm* __restrict__ gs) {
     const double* Bs = As + GKC * GLD2;
 #pragma unroll
     for (int kk = 0; kk < GKC / 4; ++kk) {
-      const int k = kk * 4 + fk;
-      const double a0 = As[k * GLD2 + 32 * wr + fr], a1 = As[k * GLD2 + 32 * wr + 16 + fr];
+      const int k = kk * 4 + fk, sa = TA ? k >> 1 : 0, sb = TB ? 0 : k >> 1;
+      const double a0 = As[k * GLD2 + ((32 * wr + fr) ^ sa)], a1 = As[k * GLD2 + ((32 * wr + 16 + fr) ^ sa)];
       double b[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = Bs[k * GLD2 + 64 * wc + 16 * q + fr];
+      for (int q = 0; q < 4; ++q) b[q] = Bs[k * GLD2 + ((64 * wc + 16 * q + fr) ^ sb)];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         acc.c[0][q] = MFMA64(a0, b[q], acc.c[0][q]);
