@@ -1055,14 +1055,16 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
     // (1) G = Z_p' Z_p: wave w sums the 16-row blocks 16 (w + 4 j), 4 k-steps per batch
     Quad acc;
     quad_zero(acc);
-    for (int i0 = 16 * w; i0 < M; i0 += 16 * (MG_T / 64)) {
-      double a0[4], a1[4];
+    // two row blocks per step: 16 loads per lane in flight
+    auto gload = [&](int i0, double (&a0)[4], double (&a1)[4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = i0 + 4 * u + fk;
         a0[u] = bload(rz, i < M && fr < nb, i + ld * fr);
         a1[u] = bload(rz, i < M && 16 + fr < nb, i + ld * (16 + fr));
       }
+    };
+    auto gmfma = [&](const double (&a0)[4], const double (&a1)[4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         acc.c[0][0] = MFMA64(a0[u], a0[u], acc.c[0][0]);
@@ -1070,6 +1072,13 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
         acc.c[1][0] = MFMA64(a1[u], a0[u], acc.c[1][0]);
         acc.c[1][1] = MFMA64(a1[u], a1[u], acc.c[1][1]);
       }
+    };
+    for (int i0 = 16 * w; i0 < M; i0 += 2 * 16 * (MG_T / 64)) {
+      double a0[4], a1[4], b0[4], b1[4];
+      gload(i0, a0, a1);
+      gload(i0 + 16 * (MG_T / 64), b0, b1);  // past M: masked, loads 0 (adds +0 products)
+      gmfma(a0, a1);
+      gmfma(b0, b1);
     }
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
@@ -1133,13 +1142,20 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
     for (int kk = 0; kk < TNB / 4; ++kk)
 #pragma unroll
       for (int nbk = 0; nbk < 2; ++nbk) rb[nbk][kk] = Ri[(4 * kk + fk) + RL * (16 * nbk + fr)];
-    for (int i0 = 16 * w; i0 < M; i0 += 16 * (MG_T / 64)) {
-      double za[TNB / 4];
+    // the next row block's loads are issued before this block's stores (the
+    // compiler cannot move them past stores into the same buffer itself)
+    double za[TNB / 4];
+    auto zload = [&](int i0, double (&z)[TNB / 4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int kk = 0; kk < TNB / 4; ++kk) {
         const int i = i0 + fr, a = 4 * kk + fk;
-        za[kk] = bload(rz, i < M && a < nb, i + ld * a);
+        z[kk] = bload(rz, i < M && a < nb, i + ld * a);
       }
+    };
+    zload(16 * w, za);
+    for (int i0 = 16 * w; i0 < M; i0 += 16 * (MG_T / 64)) {
+      double zn[TNB / 4];
+      zload(i0 + 16 * (MG_T / 64), zn);  // past M: masked, loads 0
       d4 o0 = (d4){0.0, 0.0, 0.0, 0.0}, o1 = o0;
 #pragma unroll
       for (int kk = 0; kk < TNB / 4; ++kk) {
@@ -1154,6 +1170,8 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
           if (16 + c < nb) Z[i + ld * (16 + c)] = o1[rr];
         }
       }
+#pragma unroll
+      for (int kk = 0; kk < TNB / 4; ++kk) za[kk] = zn[kk];
     }
     __syncthreads();
   }
