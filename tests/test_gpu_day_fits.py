@@ -1,5 +1,5 @@
 """T3 on the HEADLINE's own cells: the
-GPU's GPR3D(opt=True) fits of 232 cells of the bench day itself
+GPU's GPR3D(opt=True) fits of 360 cells of the bench day itself
 (``synthetic.make_day(seed=0)``, the day `bench.py` times) against the
 REFERENCE's own fits of the same cells (tests/golden/day_ref_fits.npz, made by
 tests/golden/make_day_fits.py running GPR_CS2S3.py:143-191 -- CG at :166 --
@@ -11,7 +11,7 @@ count, and (round 5) 16 more in every bucket from 600 to 3000 (128), so that
 n >= 600 holds 192 cells.  Both site forms are fitted: ``OI_DEDUP=1`` (the default, the m x m
 duplicate-site form) and ``OI_DEDUP=0`` (the plain n x n form).
 
-Rules (232 samples, no slack cells), each also as a statistical test of the
+Rules (360 samples, no slack cells), each also as a statistical test of the
 hypothesis they stand for -- the GPU fit is one more observation order of
 the reference -- since two noisy counts over the same cells are
 not ordered by an unbiased fit:
