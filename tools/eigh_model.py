@@ -11,7 +11,8 @@ kernels run.
   2. eigenvalues of the tridiagonal by bisection on Sturm counts (dstebz);
   3. eigenvectors of the tridiagonal by inverse iteration with partial
      pivoting (dlagtf / dlagts), a pseudo-random start per eigenvalue;
-  4. block classical Gram-Schmidt twice (BCGS2) over panels of 32 vectors,
+  4. block classical Gram-Schmidt twice (BCGS2) over blocks of 128 and
+     panels of 32 vectors,
      Cholesky QR twice inside a panel; where a column collapses (numerically
      repeated eigenvalues) Gram-Schmidt column by column with a fresh start
      vector;
@@ -56,10 +57,13 @@ def sytrd(A0, nbt=NBT):
             L = np.tril(A[g + 1:, g + 1:])
             A22 = L + np.tril(L, -1).T
             y = A22 @ v[g + 1:]
-            y -= V[g + 1:, :i] @ (W[g + 1:, :i].T @ v[g + 1:]) + W[g + 1:, :i] @ (V[g + 1:, :i].T @ v[g + 1:])
+            wv_, vv_ = W[g + 1:, :i].T @ v[g + 1:], V[g + 1:, :i].T @ v[g + 1:]
+            # w'v from the dots (round 5, k_sy_w: no reduction over w):
+            # w'v = tau (y'v - 2 (W'v).(V'v))
+            a2 = -0.5 * t * (t * (y @ v[g + 1:] - 2.0 * (wv_ @ vv_)))
+            y -= V[g + 1:, :i] @ wv_ + W[g + 1:, :i] @ vv_
             w = np.zeros(M)
-            w[g + 1:] = t * y
-            w[g + 1:] += (-0.5 * t * (w[g + 1:] @ v[g + 1:])) * v[g + 1:]
+            w[g + 1:] = t * y + a2 * v[g + 1:]
             V[:, i], W[:, i] = v, w
         # trailing update (rows / columns from p + nb)
         q = p + nb
@@ -223,16 +227,28 @@ def cholqr2(Z, p, q):
     return True
 
 
-def bcgs2(Z, nb=32):
+def bcgs2(Z, nb=32, ob=128):
+    """Two-level BCGS2 (round 5, OI_ORTH_BLOCK = ob): each ob-column block
+    projected out of every earlier block twice, then BCGS2 between its
+    nb-column panels; ob = nb is plain panel-wise BCGS2."""
     M, K = Z.shape
     Z = Z.copy()
-    for p in range(0, K, nb):
-        q = min(K, p + nb)
+
+    def project(lo, p, q):
         for _ in range(2):
-            H = Z[:, :p].T @ Z[:, p:q]
-            Z[:, p:q] -= Z[:, :p] @ H
-        if not cholqr2(Z, p, q):
-            mgs(Z, p, q)
+            H = Z[:, lo:p].T @ Z[:, p:q]
+            Z[:, p:q] -= Z[:, lo:p] @ H
+
+    for P in range(0, K, ob):
+        Q = min(K, P + ob)
+        if P > 0:
+            project(0, P, Q)
+        for p in range(P, Q, nb):
+            q = min(K, p + nb)
+            if p > P:
+                project(P, p, q)
+            if not cholqr2(Z, p, q):
+                mgs(Z, p, q)
     return Z
 
 
