@@ -612,14 +612,28 @@ __global__ __launch_bounds__(SW_T) void k_sy_w(const Eigh* __restrict__ es, int 
   __shared__ double pan[2 * TNB];
   __shared__ double rowg1[2 * TNB + 1];  // W(g+1, q), V(g+1, q) for q < i; w_i(g+1)
   const Eigh E = es[blockIdx.x];
-  const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i;
+  const int M = E.M, ld = E.lda, t = threadIdx.x, g = p + i, g1 = g + 1;
   if (g >= M - 1) return;
   const int r = g + 1 + SW_T * blockIdx.y + t;
   if (g + 1 + SW_T * blockIdx.y >= M) return;  // no rows for this workgroup (uniform)
   EighWsG ws = carveG(E.work, M);
   const Rsrc rV = rsrc(carve(E.work, M).Vc + (size_t)M * p), rW = rsrc(carve(E.work, M).Ws);
+  const bool upd = next && g1 < M - 1;
+  // this thread's row of the panel's V and W, loaded once for w and for the
+  // next column's update (all TNB columns in flight; q >= i loads 0, and the
+  // sums below subtract exactly +0 there, so they equal the q < i sums)
+  double vr[TNB], wr[TNB];
+#pragma unroll
+  for (int q = 0; q < TNB; ++q) {
+    vr[q] = bload(rV, q < i && r < M, (size_t)M * q + r);
+    wr[q] = bload(rW, q < i && r < M, (size_t)M * q + r);
+  }
   const double tau = ws.tau[g];
   if (t < 2 * TNB) pan[t] = t % TNB < i ? ws.X[t] : 0.0;
+  if (upd && t < TNB) {  // zeros from i on
+    rowg1[t] = t < i ? ws.Ws[(size_t)M * t + g1] : 0.0;
+    rowg1[TNB + t] = t < i ? ws.Vc[(size_t)M * (p + t) + g1] : 0.0;
+  }
   __syncthreads();
   // w'v = tau (y'v - 2 (W'v).(V'v)), fixed order
   double yv = 0.0, dd = 0.0;
@@ -628,18 +642,6 @@ __global__ __launch_bounds__(SW_T) void k_sy_w(const Eigh* __restrict__ es, int 
   const double a2 = -0.5 * tau * (tau * (yv - 2.0 * dd));
   const gdouble* vgc = ws.Vc + (size_t)M * g;
   // w_i(row) = tau (y - V(row,:) W'v - W(row,:) V'v) + a2 v(row)
-  auto wrow = [&](int rr) {
-    double sa = 0.0;
-    for (int s = 0; s < ns; ++s) sa += ws.H[(size_t)s * M + rr];
-    // all TNB columns' loads in flight at once; q >= i loads 0 against pan = 0,
-    // and sa - (+0) == sa for every sa, so the sum is the q < i one exactly
-#pragma unroll
-    for (int q = 0; q < TNB; ++q) {
-      const double va = bload(rV, q < i, (size_t)M * q + rr), wa = bload(rW, q < i, (size_t)M * q + rr);
-      sa -= va * pan[q] + wa * pan[TNB + q];
-    }
-    return tau * sa + a2 * vgc[rr];
-  };
   gdouble* wcol = ws.Ws + (size_t)M * i;
   if (blockIdx.y == 0) {
     // column i of the block reflector's T (dlarft, forward columnwise), in the
@@ -659,28 +661,29 @@ __global__ __launch_bounds__(SW_T) void k_sy_w(const Eigh* __restrict__ es, int 
     }
     for (int rr = t; rr <= g && rr < M; rr += SW_T) wcol[rr] = 0.0;
   }
+  if (upd && t == 0) {  // w_i(g1), for this workgroup's update (as the row formula below)
+    double sa = 0.0;
+    for (int s = 0; s < ns; ++s) sa += ws.H[(size_t)s * M + g1];
+    for (int q = 0; q < i; ++q) sa -= ws.Vc[(size_t)M * (p + q) + g1] * pan[q] + ws.Ws[(size_t)M * q + g1] * pan[TNB + q];
+    rowg1[2 * TNB] = tau * sa + a2 * vgc[g1];
+  }
   double w = 0.0;
   if (r < M) {
-    w = wrow(r);
+    double sa = 0.0;
+    for (int s = 0; s < ns; ++s) sa += ws.H[(size_t)s * M + r];
+#pragma unroll
+    for (int q = 0; q < TNB; ++q) sa -= vr[q] * pan[q] + wr[q] * pan[TNB + q];
+    w = tau * sa + a2 * vgc[r];
     wcol[r] = w;
   }
-  if (!next || g + 1 >= M - 1) return;
-  // column g1 = g + 1, rows >= g1: A(r,g1) -= V(r,q) W(g1,q) + W(r,q) V(g1,q), q <= i
-  const int g1 = g + 1;
-  if (t < TNB) {  // zeros from i on (the masked loop below adds exactly +0 there)
-    rowg1[t] = t < i ? ws.Ws[(size_t)M * t + g1] : 0.0;
-    rowg1[TNB + t] = t < i ? ws.Vc[(size_t)M * (p + t) + g1] : 0.0;
-  }
-  if (t == 0) rowg1[2 * TNB] = wrow(g1);
+  if (!upd) return;
   __syncthreads();
+  // column g1, rows >= g1: A(r,g1) -= V(r,q) W(g1,q) + W(r,q) V(g1,q), q <= i
   if (r < M) {
     gdouble* A = G(E.A);
     double sa = A[r + (size_t)ld * g1];
 #pragma unroll
-    for (int q = 0; q < TNB; ++q) {
-      const double va = bload(rV, q < i, (size_t)M * q + r), wa = bload(rW, q < i, (size_t)M * q + r);
-      sa -= va * rowg1[q] + wa * rowg1[TNB + q];
-    }
+    for (int q = 0; q < TNB; ++q) sa -= vr[q] * rowg1[q] + wr[q] * rowg1[TNB + q];
     sa -= vgc[r] * rowg1[2 * TNB] + w * vgc[g1];  // q = i: W(g1, i), V(g1, i) = v_g(g1)
     A[r + (size_t)ld * g1] = sa;
   }
