@@ -1103,42 +1103,56 @@ __global__ __launch_bounds__(MG_T) void k_orth_panel(const Eigh* __restrict__ es
       if (a == b) gd[a] = g;
     }
     __syncthreads();
-    // (2) G = R'R (upper R, right-looking, row j scaled by its pivot)
-    for (int j = 0; j < nb; ++j) {
-      if (t == 0) {
-        const double dj = R[j + RL * j];
-        if (!(dj > 1e-4 * gd[j])) bad = 1;
-        R[j + RL * j] = sqrt(fmax(dj, 1e-300));
+    // (2) G = R'R (upper R, right-looking, row j scaled by its pivot) and
+    // (3) R^-1, both in wave 0's registers: lane c holds column c (g[k] = row
+    // k), rows of R broadcast by lane reads -- the same operations in the same
+    // order as the LDS form with three block barriers per column it replaces
+    if (w == 0) {
+      const int c = lane;
+      double g[TNB];
+#pragma unroll
+      for (int k = 0; k < TNB; ++k) g[k] = c < TNB ? R[k + RL * c] : 0.0;
+      bool badl = false;
+#pragma unroll
+      for (int j = 0; j < TNB; ++j) {
+        if (j < nb) {  // uniform
+          const double dj = __shfl(g[j], j, 64);
+          if (!(dj > 1e-4 * gd[j])) badl = true;
+          const double rjj = sqrt(fmax(dj, 1e-300));
+          const double inv = 1.0 / rjj;
+          if (c == j) g[j] = rjj;
+          else if (c > j && c < nb) g[j] *= inv;
+#pragma unroll
+          for (int b = j + 1; b < TNB; ++b) {
+            const double rjb = __shfl(g[j], b, 64);  // R(j, b)
+            if (b < nb && c >= b && c < nb) g[b] -= rjb * g[j];
+          }
+        }
       }
-      __syncthreads();
-      const double inv = 1.0 / R[j + RL * j];
-      for (int l = j + 1 + t; l < nb; l += MG_T) R[j + RL * l] *= inv;
-      __syncthreads();
-      const int L = nb - j - 1;
-      for (int e = t; e < L * L; e += MG_T) {
-        const int a = j + 1 + e % L, b = j + 1 + e / L;
-        if (a <= b) R[a + RL * b] -= R[j + RL * a] * R[j + RL * b];
+      if (c < TNB)
+#pragma unroll
+        for (int k = 0; k < TNB; ++k) R[k + RL * c] = g[k];
+      if (lane == 0) bad = badl;
+      // R^-1 (upper), lane l = column l: x_a = (delta_al - sum_{k>a} R(a,k) x_k) / R(a,a);
+      // x_k = +0 for k > l and past nb, so the sums are the k <= l ones exactly
+      if (!badl && c < TNB) {
+        double x[TNB];
+#pragma unroll
+        for (int aa = TNB - 1; aa >= 0; --aa) {
+          double sx = aa == c ? 1.0 : 0.0;
+#pragma unroll
+          for (int k = aa + 1; k < TNB; ++k) sx -= R[aa + RL * k] * x[k];
+          x[aa] = (aa < nb && c < nb) ? sx / R[aa + RL * aa] : 0.0;
+        }
+#pragma unroll
+        for (int aa = 0; aa < TNB; ++aa) Ri[aa + RL * c] = x[aa];
       }
-      __syncthreads();
     }
+    __syncthreads();
     if (bad) {  // k_mgs_panel takes the panel over
       if (t == 0) carve(E.work, M).flag[0] = 1.0;
       return;
     }
-    // (3) R^-1 (upper), one thread per column
-    if (t < TNB) {
-      const int l = t;
-      for (int a = TNB - 1; a >= 0; --a) {
-        double x = 0.0;
-        if (l < nb && a <= l) {
-          x = a == l ? 1.0 : 0.0;
-          for (int k = a + 1; k <= l; ++k) x -= R[a + RL * k] * Ri[k + RL * l];
-          x /= R[a + RL * a];
-        }
-        Ri[a + RL * l] = x;
-      }
-    }
-    __syncthreads();
     // (4) Z_p <- Z_p R^-1 on the MFMA core, wave w over the 16-row blocks 16 (w + 4 j)
     double rb[2][TNB / 4];
 #pragma unroll
