@@ -710,11 +710,13 @@ __device__ __forceinline__ double start_value(int k, int i) {
 // serial chains per thread, so the batch is spread over the whole chip.
 // dynamic LDS: d[M] | e2[M] | red[64]
 #define ST_T 64
-__device__ __forceinline__ void tri_setup(const Eigh& E, const EighWsG& ws, double* d, double* e2, double* red) {
+__device__ __forceinline__ void tri_setup(const Eigh& E, const EighWsG& ws, double* d, double* e2, double* red,
+                                          double* el = nullptr) {
   const int M = E.M, t = threadIdx.x;
   for (int i = t; i < M; i += ST_T) {
     d[i] = ws.d[i];
     e2[i] = i < M - 1 ? ws.e[i] * ws.e[i] : 0.0;
+    if (el) el[i] = i < M - 1 ? ws.e[i] : 0.0;
   }
   __syncthreads();
   if (t == 0) {  // Gershgorin interval, ||T||, pivmin (dstebz)
@@ -763,6 +765,9 @@ __global__ __launch_bounds__(ST_T) void k_stebz(const Eigh* __restrict__ es) {
       double q = d[0] - mid;
       if (fabs(q) < pivmin) q = -pivmin;
       cnt += q < 0.0;
+      // unrolled so that the LDS reads of d, e2 for 8 steps issue ahead of
+      // the division chain (one wave per SIMD here: nothing else hides them)
+#pragma unroll 8
       for (int i = 1; i < M; ++i) {
         q = d[i] - mid - e2[i - 1] / q;
         if (fabs(q) < pivmin) q = -pivmin;
@@ -787,7 +792,8 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
   double* d = sm;
   double* e2 = d + M;
   double* red = e2 + M;
-  tri_setup(E, ws, d, e2, red);
+  double* el = red + 64;  // e, for the factorisation's loads
+  tri_setup(E, ws, d, e2, red, el);
   const double tnorm = red[2];
   const double eps = 2.220446049250313e-16;
   const size_t MM = (size_t)M * M;
@@ -830,10 +836,11 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
     }
     // T - lam I = P L U (dlagtf), factors at [i * M + k]
     {
-      double ak = d[0] - lam, bk = M > 1 ? ws.e[0] : 0.0;
+      double ak = d[0] - lam, bk = M > 1 ? el[0] : 0.0;
+#pragma unroll 4
       for (int i = 0; i < M - 1; ++i) {
-        const double sub = ws.e[i];
-        const double an = d[i + 1] - lam, bn = i + 1 < M - 1 ? ws.e[i + 1] : 0.0;
+        const double sub = el[i];
+        const double an = d[i + 1] - lam, bn = i + 1 < M - 1 ? el[i + 1] : 0.0;
         double m, cnew = 0.0, a_i, b_i, a_next, b_next, piv = 0.0;
         if (fabs(ak) >= fabs(sub)) {
           m = ak != 0.0 ? sub / ak : 0.0;
@@ -875,6 +882,7 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
     for (int iter = 0; iter < 2; ++iter) {
       // forward: apply P and L
       double prev = sx[k];
+#pragma unroll 4
       for (int i = 0; i < M - 1; ++i) {
         const size_t o = (size_t)i * M + k;
         const double nx = sx[o + M];
@@ -889,6 +897,7 @@ __global__ __launch_bounds__(ST_T) void k_stein(const Eigh* __restrict__ es) {
       sx[(size_t)(M - 1) * M + k] = prev;
       // backward with U, tiny pivots perturbed (dlagts, job = -1)
       double x1 = 0.0, x2 = 0.0, amax = 0.0;
+#pragma unroll 4
       for (int i = M - 1; i >= 0; --i) {
         const size_t o = (size_t)i * M + k;
         double s = sx[o] - sb[o] * x1 - sc[o] * x2;
@@ -1390,7 +1399,7 @@ void eigh(Stager& S, hipStream_t st, const std::vector<Eigh>& es, const std::fun
   hipLaunchKernelGGL(k_sytrd_last, dim3(n), dim3(64), 0, st, de);
   LC(hipGetLastError());
   phase(1);
-  const size_t lds_st = (2 * (size_t)Mmax + 64) * sizeof(double);
+  const size_t lds_st = (3 * (size_t)Mmax + 64) * sizeof(double);  // d | e2 | red[64] | e (k_stein)
   const unsigned nst = (unsigned)((Mmax + ST_T - 1) / ST_T), nto = (unsigned)((Mmax + 63) / 64);
   hipLaunchKernelGGL(k_stebz, dim3(n, nst), dim3(ST_T), lds_st, st, de);
   LC(hipGetLastError());

@@ -1,5 +1,5 @@
-# round 5: (1) k_sy_w loads its row of the panel's V and W once; (2) k_orth_panel's
-# Cholesky QR in wave 0's registers: probe (eigenpairs must be unchanged), Nystrom tests, line
+# round 5: k_sy_w rows once; k_orth_panel Cholesky QR in registers; stebz / stein loops unrolled (LDS e):
+# probe (eigenpairs must be unchanged), Nystrom tests, line
 set -o pipefail
 D=gpurun_out/r05/${TAG:-z}; mkdir -p $D
 timeout -k 10 180 tools/eigh_probe 928 64 > $D/eigh_probe.txt 2>&1 || { cat $D/eigh_probe.txt; exit 1; }
