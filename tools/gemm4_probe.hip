@@ -17,7 +17,7 @@ __device__ __forceinline__ const double* tile(const double* X, int mode, int wg,
 
 struct Acc8 { d4 c[2][4]; };
 
-template <int LDSS>
+template <int LDSS, int SCHED = 0>
 __global__ __launch_bounds__(512) void g4(const double* A, const double* B, double* C, int P, int mode) {
   constexpr int STG = KC * LDSS;  // one 16 x 128 operand chunk
   __shared__ __attribute__((aligned(16))) double lds[4 * STG];
@@ -58,6 +58,25 @@ __global__ __launch_bounds__(512) void g4(const double* A, const double* B, doub
         acc.c[0][q] = MFMA64(a0, b[q], acc.c[0][q]);
         acc.c[1][q] = MFMA64(a1, b[q], acc.c[1][q]);
       }
+    }
+    // SCHED: interleave the chunk's 24 LDS reads with its 32 MFMAs (mask 0x100
+    // DS read, 0x008 MFMA) instead of the compiler's grouping
+    if (SCHED == 1) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+      for (int i = 0; i < 18; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 14, 0);
+    } else if (SCHED == 2) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
     }
   };
   load(0, r0);
@@ -294,6 +313,7 @@ int main() {
       for (size_t i = 0; i < h.size(); ++i) bad += h[i] != ref[i];
       printf("check %-16s %zu of %zu differ\n", name, bad, h.size());
     };
+    chk("g4 sched1", g4<144, 1>); chk("g4 sched2", g4<144, 2>);
     chk("g4g kc16 nbuf2", g4g<16, 2>); chk("g4g kc16 nbuf3", g4g<16, 3>); chk("g4g kc8 nbuf4", g4g<8, 4>);
     chk("g4g kc8 nbuf3", g4g<8, 3>); chk("g4g kc32 nbuf2", g4g<32, 2>);
   }
@@ -312,12 +332,18 @@ int main() {
   run("g1 64x64", g1, 256, 4 * nwg, tp);
   run("g2 64x128", g2, 512, 2 * nwg, 2 * tp);
   run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
+  run("g4 s144 sched1", g4<144, 1>, 512, nwg, 4 * tp);
+  run("g4 s144 sched2", g4<144, 2>, 512, nwg, 4 * tp);
+  run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
   run("g4 128x128 s136", g4<136>, 512, nwg, 4 * tp);
   run("g4g kc16 nbuf2", g4g<16, 2>, 512, nwg, 4 * tp);
   run("g4g kc16 nbuf3", g4g<16, 3>, 512, nwg, 4 * tp);
   run("g4g kc8 nbuf4", g4g<8, 4>, 512, nwg, 4 * tp);
   run("g4g kc8 nbuf3", g4g<8, 3>, 512, nwg, 4 * tp);
   run("g4g kc32 nbuf2", g4g<32, 2>, 512, nwg, 4 * tp);
+  run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
+  run("g4 s144 sched1", g4<144, 1>, 512, nwg, 4 * tp);
+  run("g4 s144 sched2", g4<144, 2>, 512, nwg, 4 * tp);
   run("g4 128x128 s144", g4<144>, 512, nwg, 4 * tp);
   run("g8 256x128 regs", (g8<false, 2>), 512, nwg / 2, 8 * tp);
   run("g8 256x128 glds2", (g8<true, 2>), 512, nwg / 2, 8 * tp);
