@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
 #define GT2 128
 #define GLD2 144
 template <bool TA, bool TB>
-__global__ __launch_bounds__(512) void k_gemm128(const Gemm* __restrict__ gs) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_gemm128(const Gemm* __restrict__ gs) {
   __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GKC * GLD2];
   const Gemm g = gs[blockIdx.y];
   const int tm = (g.m + GT2 - 1) / GT2, tn = (g.n + GT2 - 1) / GT2;
@@ -207,32 +207,62 @@ __global__ __launch_bounds__(512) void k_gemm128(const Gemm* __restrict__ gs) {
   Quad8 acc;
   quad8_zero(acc);
   const int nch = (kmax + GKC - 1) / GKC;
-  double ra[4], rb[4];
+  const bool edge_mn = m0 + GT2 > g.m || n0 + GT2 > g.n;
+  // staged as element pairs along each operand's contiguous dimension: pair
+  // p = t + 512 q of a 128 x 16 chunk -- k-contiguous (A with TA, B without
+  // TB): k = 2 (p & 7), row p >> 3; otherwise k = p >> 6, rows 2 (p & 63), +1.
+  // Interior chunks load a pair with one 16-byte buffer load; chunks at the
+  // matrix edges load its two elements masked.
+  dv2 pa[2], pb[2];
   const Rsrc rA = rsrc(g.A), rB = rsrc(g.B);
-  // element e = t + 512 q of a 128 x 16 chunk: A(m, k) and op(B)(k, n)
+  auto pair_load = [](Rsrc r, bool full, bool ok0, bool ok1, size_t idx) __attribute__((always_inline)) {
+    if (full) return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(idx * 8), 0, 0));
+    return dv2{bload(r, ok0, idx), bload(r, ok1, idx + 1)};
+  };
   auto load = [&](int ch) __attribute__((always_inline)) {
     const int k0 = ch * GKC;
+    const bool full = !edge_mn && k0 + GKC <= kmax;  // uniform
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = t + 512 * q;
-      int m, k;
-      if (TA) { k = e & 15; m = e >> 4; } else { m = e & 127; k = e >> 7; }
-      const int gm = m0 + m, gk = k0 + k;
-      ra[q] = bload(rA, gm < g.m && gk < kmax, TA ? gk + (size_t)g.lda * gm : gm + (size_t)g.lda * gk);
-      int n, kb;
-      if (TB) { n = e & 127; kb = e >> 7; } else { kb = e & 15; n = e >> 4; }
-      const int gn = n0 + n, gkb = k0 + kb;
-      rb[q] = bload(rB, gn < g.n && gkb < kmax, TB ? gn + (size_t)g.ldb * gkb : gkb + (size_t)g.ldb * gn);
+    for (int q = 0; q < 2; ++q) {
+      const int pp = t + 512 * q;
+      if (TA) {
+        const int gk = k0 + 2 * (pp & 7), gm = m0 + (pp >> 3);
+        pa[q] = pair_load(rA, full, gm < g.m && gk < kmax, gm < g.m && gk + 1 < kmax, gk + (size_t)g.lda * gm);
+      } else {
+        const int gm = m0 + 2 * (pp & 63), gk = k0 + (pp >> 6);
+        pa[q] = pair_load(rA, full, gm < g.m && gk < kmax, gm + 1 < g.m && gk < kmax, gm + (size_t)g.lda * gk);
+      }
+      if (TB) {
+        const int gn = n0 + 2 * (pp & 63), gk = k0 + (pp >> 6);
+        pb[q] = pair_load(rB, full, gn < g.n && gk < kmax, gn + 1 < g.n && gk < kmax, gn + (size_t)g.ldb * gk);
+      } else {
+        const int gk = k0 + 2 * (pp & 7), gn = n0 + (pp >> 3);
+        pb[q] = pair_load(rB, full, gn < g.n && gk < kmax, gn < g.n && gk + 1 < kmax, gk + (size_t)g.ldb * gn);
+      }
     }
   };
+  // k-contiguous operands sit at column m ^ 4 (k >> 1): the pair stores of a
+  // half-wave (8 k-pairs x 4 rows) and the compute reads stay conflict-free
   auto store = [&](int buf) __attribute__((always_inline)) {
     double* As = lds + buf * 2 * GKC * GLD2;
     double* Bs = As + GKC * GLD2;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = t + 512 * q;
-      if (TA) As[(e & 15) * GLD2 + ((e >> 4) ^ ((e & 15) >> 1))] = ra[q]; else As[(e >> 7) * GLD2 + (e & 127)] = ra[q];
-      if (TB) Bs[(e >> 7) * GLD2 + (e & 127)] = rb[q]; else Bs[(e & 15) * GLD2 + ((e >> 4) ^ ((e & 15) >> 1))] = rb[q];
+    for (int q = 0; q < 2; ++q) {
+      const int pp = t + 512 * q;
+      if (TA) {
+        const int k = 2 * (pp & 7), m = (pp >> 3) ^ ((k >> 1) << 2);
+        As[k * GLD2 + m] = pa[q].x;
+        As[(k + 1) * GLD2 + m] = pa[q].y;
+      } else {
+        *(dv2*)(As + (pp >> 6) * GLD2 + 2 * (pp & 63)) = pa[q];
+      }
+      if (TB) {
+        *(dv2*)(Bs + (pp >> 6) * GLD2 + 2 * (pp & 63)) = pb[q];
+      } else {
+        const int k = 2 * (pp & 7), n = (pp >> 3) ^ ((k >> 1) << 2);
+        Bs[k * GLD2 + n] = pb[q].x;
+        Bs[(k + 1) * GLD2 + n] = pb[q].y;
+      }
     }
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
@@ -240,7 +270,7 @@ __global__ __launch_bounds__(512) void k_gemm128(const Gemm* __restrict__ gs) {
     const double* Bs = As + GKC * GLD2;
 #pragma unroll
     for (int kk = 0; kk < GKC / 4; ++kk) {
-      const int k = kk * 4 + fk, sa = TA ? k >> 1 : 0, sb = TB ? 0 : k >> 1;
+      const int k = kk * 4 + fk, sa = TA ? (k >> 1) << 2 : 0, sb = TB ? 0 : (k >> 1) << 2;
       const double a0 = As[k * GLD2 + ((32 * wr + fr) ^ sa)], a1 = As[k * GLD2 + ((32 * wr + 16 + fr) ^ sa)];
       double b[4];
 #pragma unroll
