@@ -88,11 +88,21 @@ __device__ __forceinline__ double bload(Rsrc r, bool ok, size_t idx) {
 #define GT 64
 #define GKC 16
 #define GLD 80  // LDS row stride of a staged 16 x 64 chunk (rows k, k+1 in opposite bank halves)
-// A k-contiguous operand (A with TA, B without TB) is stored transposed: the
-// 16 lanes of a half-wave that hold one m and k = 0 .. 15 would hit two banks
-// (8-way conflicts), so element (k, m) sits at column m ^ (k >> 1) -- a
-// permutation inside m's aligned 8-block; the compute reads apply the same XOR
-// and stay conflict-free (k >> 1 is uniform across a half-wave's lanes).
+// Operands are staged as element pairs along their contiguous dimension (one
+// 16-byte buffer load per pair on interior chunks, two masked 8-byte loads at
+// the matrix edges).  A k-contiguous operand (A with TA, B without TB) is
+// stored transposed: a half-wave holds 8 k-pairs of 4 rows, and plain
+// placement would put its even rows on two banks (8-way conflicts), so element
+// (k, m) sits at column m ^ 4 (k >> 1) -- a permutation inside m's aligned
+// 32-block; the compute reads apply the same XOR and stay conflict-free
+// (k >> 1 is uniform across a half-wave's lanes).
+
+// elements idx, idx + 1: one 16-byte load when `full` (uniform), else two
+// masked 8-byte loads
+__device__ __forceinline__ dv2 pair_load(Rsrc r, bool full, bool ok0, bool ok1, size_t idx) {
+  if (full) return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(idx * 8), 0, 0));
+  return dv2{bload(r, ok0, idx), bload(r, ok1, idx + 1)};
+}
 
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
@@ -110,32 +120,53 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
   Quad acc;
   quad_zero(acc);
   const int nch = (kmax + GKC - 1) / GKC;
-  double ra[4], rb[4];
+  const bool edge_mn = m0 + GT > g.m || n0 + GT > g.n;
+  // pair p = t + 256 q of a 64 x 16 chunk: k-contiguous k = 2 (p & 7), row
+  // p >> 3; otherwise k = p >> 5, rows 2 (p & 31), +1
+  dv2 pa[2], pb[2];
   const Rsrc rA = rsrc(g.A), rB = rsrc(g.B);
-  // element e = t + 256 q of a 64 x 16 chunk: A(m, k) and op(B)(k, n)
   auto load = [&](int ch) __attribute__((always_inline)) {
     const int k0 = ch * GKC;
+    const bool full = !edge_mn && k0 + GKC <= kmax;  // uniform
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = t + 256 * q;
-      int m, k;
-      if (TA) { k = e & 15; m = e >> 4; } else { m = e & 63; k = e >> 6; }
-      const int gm = m0 + m, gk = k0 + k;
-      ra[q] = bload(rA, gm < g.m && gk < kmax, TA ? gk + (size_t)g.lda * gm : gm + (size_t)g.lda * gk);
-      int n, kb;
-      if (TB) { n = e & 63; kb = e >> 6; } else { kb = e & 15; n = e >> 4; }
-      const int gn = n0 + n, gkb = k0 + kb;
-      rb[q] = bload(rB, gn < g.n && gkb < kmax, TB ? gn + (size_t)g.ldb * gkb : gkb + (size_t)g.ldb * gn);
+    for (int q = 0; q < 2; ++q) {
+      const int pp = t + 256 * q;
+      if (TA) {
+        const int gk = k0 + 2 * (pp & 7), gm = m0 + (pp >> 3);
+        pa[q] = pair_load(rA, full, gm < g.m && gk < kmax, gm < g.m && gk + 1 < kmax, gk + (size_t)g.lda * gm);
+      } else {
+        const int gm = m0 + 2 * (pp & 31), gk = k0 + (pp >> 5);
+        pa[q] = pair_load(rA, full, gm < g.m && gk < kmax, gm + 1 < g.m && gk < kmax, gm + (size_t)g.lda * gk);
+      }
+      if (TB) {
+        const int gn = n0 + 2 * (pp & 31), gk = k0 + (pp >> 5);
+        pb[q] = pair_load(rB, full, gn < g.n && gk < kmax, gn + 1 < g.n && gk < kmax, gn + (size_t)g.ldb * gk);
+      } else {
+        const int gk = k0 + 2 * (pp & 7), gn = n0 + (pp >> 3);
+        pb[q] = pair_load(rB, full, gn < g.n && gk < kmax, gn < g.n && gk + 1 < kmax, gk + (size_t)g.ldb * gn);
+      }
     }
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
     double* As = lds + buf * 2 * GKC * GLD;
     double* Bs = As + GKC * GLD;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = t + 256 * q;
-      if (TA) As[(e & 15) * GLD + ((e >> 4) ^ ((e & 15) >> 1))] = ra[q]; else As[(e >> 6) * GLD + (e & 63)] = ra[q];
-      if (TB) Bs[(e >> 6) * GLD + (e & 63)] = rb[q]; else Bs[(e & 15) * GLD + ((e >> 4) ^ ((e & 15) >> 1))] = rb[q];
+    for (int q = 0; q < 2; ++q) {
+      const int pp = t + 256 * q;
+      if (TA) {
+        const int k = 2 * (pp & 7), m = (pp >> 3) ^ ((k >> 1) << 2);
+        As[k * GLD + m] = pa[q].x;
+        As[(k + 1) * GLD + m] = pa[q].y;
+      } else {
+        *(dv2*)(As + (pp >> 5) * GLD + 2 * (pp & 31)) = pa[q];
+      }
+      if (TB) {
+        *(dv2*)(Bs + (pp >> 5) * GLD + 2 * (pp & 31)) = pb[q];
+      } else {
+        const int k = 2 * (pp & 7), n = (pp >> 3) ^ ((k >> 1) << 2);
+        Bs[k * GLD + n] = pb[q].x;
+        Bs[(k + 1) * GLD + n] = pb[q].y;
+      }
     }
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
@@ -143,7 +174,7 @@ __global__ __launch_bounds__(256) void k_gemm(const Gemm* __restrict__ gs) {
     const double* Bs = As + GKC * GLD;
 #pragma unroll
     for (int kk = 0; kk < GKC / 4; ++kk) {
-      const int k = kk * 4 + fk, sa = TA ? k >> 1 : 0, sb = TB ? 0 : k >> 1;
+      const int k = kk * 4 + fk, sa = TA ? (k >> 1) << 2 : 0, sb = TB ? 0 : (k >> 1) << 2;
       const double a0 = As[k * GLD + ((32 * wr + fr) ^ sa)], a1 = As[k * GLD + ((32 * wr + 16 + fr) ^ sa)];
       const double b0 = Bs[k * GLD + ((32 * wc + fr) ^ sb)], b1 = Bs[k * GLD + ((32 * wc + 16 + fr) ^ sb)];
       acc.c[0][0] = MFMA64(a0, b0, acc.c[0][0]);
@@ -215,10 +246,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   // matrix edges load its two elements masked.
   dv2 pa[2], pb[2];
   const Rsrc rA = rsrc(g.A), rB = rsrc(g.B);
-  auto pair_load = [](Rsrc r, bool full, bool ok0, bool ok1, size_t idx) __attribute__((always_inline)) {
-    if (full) return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(idx * 8), 0, 0));
-    return dv2{bload(r, ok0, idx), bload(r, ok1, idx + 1)};
-  };
   auto load = [&](int ch) __attribute__((always_inline)) {
     const int k0 = ch * GKC;
     const bool full = !edge_mn && k0 + GKC <= kmax;  // uniform

@@ -1,8 +1,8 @@
-# round 5: k_gemm128 staged as element pairs (16-byte buffer loads on
+# round 5: k_gemm128 (and since the second run k_gemm) staged as element pairs (16-byte buffer loads on
 # interior chunks, swizzle m ^ 4 (k >> 1)): GEMM probe, eigensolver probe,
 # Nystrom tests (the 64 / 128 bitwise test included) and line
 set -o pipefail
-D=gpurun_out/r05/aa; mkdir -p $D
+D=gpurun_out/r05/${TAG:-aa}; mkdir -p $D
 for g in 1 0; do OI_GEMM128=$g timeout -k 10 60 tools/gemm_probe 4600 928 32 | sed "s/^/pairs gemm128=$g /" | tee -a $D/gemm_probe.txt; done
 timeout -k 10 180 tools/eigh_probe 928 64 > $D/eigh_probe.txt 2>&1 || { cat $D/eigh_probe.txt; exit 1; }
 echo "probe: $(tr '\n' ' ' < $D/eigh_probe.txt)"
