@@ -15,7 +15,10 @@ def pytest_configure(config):
     # pytest-xdist workers: one BLAS thread each.  Several workers each running
     # a full OpenBLAS thread pool on the same CPUs turn the oracle's many small
     # solves into spin-wait contention (test_cg_trace_bitwise: 4.5 s alone,
-    # 640 s under -n 4); results are bitwise the same either way.
+    # 640 s under -n 4).  The bitwise golden checks (test_smlii_bitwise,
+    # test_day_two_ranks_equals_one) were made with OpenBLAS's default thread
+    # count and do NOT hold at one thread: run those without -n (the driver
+    # runs the suite serially).
     if os.environ.get('PYTEST_XDIST_WORKER'):
         try:
             from threadpoolctl import threadpool_limits
