@@ -982,14 +982,16 @@ def main():
     if local >= ndev and backend != 'gloo':
         raise SystemExit(f"bench.py: LOCAL_RANK {local} but {ndev} GPU(s) visible: refusing to put two "
                          f"ranks on one GPU (OI_DIST_BACKEND=gloo for a one-GPU rehearsal)")
-    if world > 1:
-        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group(backend)
     gpu = local % max(1, ndev)
     per_dev = -(-world // max(1, ndev))  # ranks sharing one GPU (the gloo rehearsal)
     if per_dev > 1:  # each rank's library arena takes a share of the HBM, not 60 % of what is left
         os.environ.setdefault('OI_ARENA_FRAC', f"{0.8 / per_dev:.4f}")
+    # the rank's device is current before the process group exists, so RCCL's
+    # communicator binds to this GPU and not to the rank-guessed default
     torch.cuda.set_device(gpu)
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group(backend)
     dev = torch.device('cuda', gpu)
     cdev = torch.device('cpu') if backend == 'gloo' else dev  # where collective tensors live
     census = rank_census(dist, torch, world, rank, gpu, cdev)
