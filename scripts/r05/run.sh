@@ -8,6 +8,8 @@
 #   multirank       tests/test_gpu_multirank.py (self-launched ranks, 2-rank bitwise)
 #   day             the driver's bench command (cpu_baseline from the day fixture)
 #   day-ab          the day back to back against $OI_LIB_BASE (new base new base)
+#   day-ab-env      the same against the knob setting $AB_ENV (e.g. AB_ENV=OI_LAUUM=4)
+#   parity-env      the GPU parity / fit / session tests under $AB_ENV
 #   day-8rank       8 self-launched gloo ranks sharing one GPU (OI_DIST_BACKEND=gloo)
 #   config1         --workload single (one n = 200 cell, GPR:166)
 #   config2         --workload predict (1000 cells x n = 500, GPR:316-319)
@@ -45,12 +47,21 @@ for step in "$@"; do
       timeout -k 10 300 python3 -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 200 --timeout-method thread > $D/multirank.log 2>&1
       rc=$?; grep -E "passed|failed" $D/multirank.log | tail -2; [ $rc -eq 0 ] ;;
     day) bench 560 day --gpus 1 --steps 20 --warmup 5 ;;
-    day-ab)
-      [ -n "$OI_LIB_BASE" ] || { echo "day-ab needs OI_LIB_BASE"; false; } &&
+    day-ab|day-ab-env)  # the day back to back: the build at $OI_LIB_BASE (day-ab) or the knob setting $AB_ENV
+      # (day-ab-env, e.g. AB_ENV=OI_LAUUM=4) against the tree's default
+      fail=0; k=0
       for leg in new base new base; do
-        if [ $leg = base ]; then export OI_LIB=$OI_LIB_BASE; else unset OI_LIB; fi
-        bench 300 day_$leg --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --parity-cells 8 || break
-      done; unset OI_LIB ;;
+        k=$((k + 1)); E=""
+        if [ $step = day-ab ]; then [ $leg = base ] && E="OI_LIB=$OI_LIB_BASE"; else [ $leg = base ] && E="$AB_ENV"; fi
+        [ $leg = base ] && [ -z "$OI_LIB_BASE$AB_ENV" ] && { echo "$step needs OI_LIB_BASE / AB_ENV"; fail=1; break; }
+        env $E timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --parity-cells 8 \
+          --out $D/day_${leg}_$k.json > $D/day_${leg}_$k.log 2>&1 || { tail -20 $D/day_${leg}_$k.log; fail=1; break; }
+        show $D/day_${leg}_$k.json "$leg($E)"
+      done; [ $fail = 0 ] ;;
+    parity-env)  # the GPU parity / fit tests under $AB_ENV
+      env $AB_ENV timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fit.py tests/test_gpu_session.py -x -q \
+        --timeout 300 --timeout-method thread > $D/parity_env.log 2>&1
+      rc=$?; tail -1 $D/parity_env.log; [ $rc -eq 0 ] || tail -30 $D/parity_env.log; [ $rc -eq 0 ] ;;
     day-8rank) OI_DIST_BACKEND=gloo bench 400 day_8rank_gloo --gpus 8 --steps 20 --warmup 2 --no-cpu-baseline --parity-cells 8 ;;
     config1) bench 300 config1 --workload single --steps 20 --warmup 3 ;;
     config2) bench 300 config2 --workload predict --steps 20 --warmup 3 ;;
