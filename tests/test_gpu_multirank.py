@@ -141,3 +141,32 @@ def test_bench_self_launch_gloo(tmp_path):
     assert line['config']['cells_total'] == 96 and line['failed_cells'] == 0
     assert line['steps'] == 4 and not line.get('truncated')
     assert line['parity']['pass'], line['parity']
+
+
+def test_bench_under_torchrun_gloo(tmp_path):
+    """The driver's N > 1 launch shape, `python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus N ...`: WORLD_SIZE comes from the launcher, bench.py starts
+    no ranks of its own, and the line reports the launcher (two gloo ranks
+    sharing the one GPU of this box)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / 'line.json'
+    env = dict(os.environ, OI_DIST_BACKEND='gloo')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT', 'OI_BENCH_LAUNCHER'):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                        '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
+                        os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '4', '--warmup', '1',
+                        '--day-cells', '96', '--no-cpu-baseline', '--parity-cells', '4', '--budget-s', '90',
+                        '--out', str(out)],
+                       env=env, capture_output=True, text=True, timeout=110, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(out.read_text())
+    assert line['n_gpus'] == 2 and line['ranks_seen'] == [0, 1] and line['rank_devices'] == [0, 0]
+    assert line['collective_backend'] == 'gloo' and line['launcher'] == 'torch.distributed.run'
+    assert line['config']['cells_total'] == 96 and line['failed_cells'] == 0
+    assert line['steps'] == 4 and not line.get('truncated')
+    assert line['parity']['pass'], line['parity']
