@@ -10,6 +10,7 @@
 #   day-ab          the day back to back against $OI_LIB_BASE (new base new base)
 #   day-ab-env      the same against the knob setting $AB_ENV (e.g. AB_ENV=OI_LAUUM=4)
 #   parity-env      the GPU parity / fit / session tests under $AB_ENV
+#   shares          config 4's 8 day shares back to back on one GPU + projection (ONE_GPU_JSON)
 #   day-8rank       8 self-launched gloo ranks sharing one GPU (OI_DIST_BACKEND=gloo)
 #   config1         --workload single (one n = 200 cell, GPR:166)
 #   config2         --workload predict (1000 cells x n = 500, GPR:316-319)
@@ -62,6 +63,14 @@ for step in "$@"; do
       env $AB_ENV timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fit.py tests/test_gpu_session.py -x -q \
         --timeout 300 --timeout-method thread > $D/parity_env.log 2>&1
       rc=$?; tail -1 $D/parity_env.log; [ $rc -eq 0 ] || tail -30 $D/parity_env.log; [ $rc -eq 0 ] ;;
+    shares)  # config 4 rehearsed on one GPU: the 8 LPT shares of the day back to back (the N = 8 depth rule),
+      # then the projection (slowest share) against the 1-GPU line $ONE_GPU_JSON
+      fail=0
+      for k in 0 1 2 3 4 5 6 7; do
+        bench 300 share_$k --gpus 1 --steps 20 --warmup 2 --day-shares 8 --share $k --no-cpu-baseline --parity-cells 0 || { fail=1; break; }
+      done
+      [ $fail = 0 ] && mkdir -p $D/shares && cp $D/share_*.json $D/shares/ &&
+      python3 scripts/r04/share_projection.py $D/shares ${ONE_GPU_JSON:-} ;;
     day-8rank) OI_DIST_BACKEND=gloo bench 400 day_8rank_gloo --gpus 8 --steps 20 --warmup 2 --no-cpu-baseline --parity-cells 8 ;;
     config1) bench 300 config1 --workload single --steps 20 --warmup 3 ;;
     config2) bench 300 config2 --workload predict --steps 20 --warmup 3 ;;
