@@ -15,16 +15,32 @@ def pytest_configure(config):
     # pytest-xdist workers: one BLAS thread each.  Several workers each running
     # a full OpenBLAS thread pool on the same CPUs turn the oracle's many small
     # solves into spin-wait contention (test_cg_trace_bitwise: 4.5 s alone,
-    # 640 s under -n 4).  The bitwise golden checks (test_smlii_bitwise,
+    # 640 s under -n 4).  The bitwise golden checks (tests/test_oracle_golden.py,
     # test_day_two_ranks_equals_one) were made with OpenBLAS's default thread
-    # count and do NOT hold at one thread: run those without -n (the driver
-    # runs the suite serially).
+    # count and do not hold at one thread: they are marked `blas_default` and
+    # run with the default count restored (fixture below).
+    config.addinivalue_line("markers", "blas_default: needs OpenBLAS's default thread count (bitwise goldens)")
     if os.environ.get('PYTEST_XDIST_WORKER'):
         try:
-            from threadpoolctl import threadpool_limits
+            from threadpoolctl import threadpool_info, threadpool_limits
+            global _BLAS_DEFAULT
+            _BLAS_DEFAULT = max((d.get('num_threads', 1) for d in threadpool_info()), default=None)
             threadpool_limits(1)
         except ImportError:
             pass
+
+
+_BLAS_DEFAULT = None
+
+
+@pytest.fixture(autouse=True)
+def _blas_default_threads(request):
+    if _BLAS_DEFAULT is None or request.node.get_closest_marker('blas_default') is None:
+        yield
+        return
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(_BLAS_DEFAULT):
+        yield
 
 
 def load_golden(name):

@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 
@@ -80,6 +81,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.blas_default
 def test_day_two_ranks_equals_one():
     from optimalinterpolation_amd import day
     world = 2

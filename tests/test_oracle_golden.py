@@ -7,6 +7,9 @@ import pytest
 from conftest import load_golden, ragged_cell
 from oracle import gp_oracle as O
 
+# bitwise against fixtures made at OpenBLAS's default thread count (conftest)
+pytestmark = pytest.mark.blas_default
+
 
 def _same(a, b):
     a = np.asarray(a, float)
