@@ -55,6 +55,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP64_TFLOPS = 78.6   # MI355X fp64 matrix (= vector) dense peak, spec
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
+LAUNCH_GRACE_S = 600.0    # launcher: ranks may run this long past --budget-s (parity check, teardown)
 METRIC = "grid-cells/sec (full GP fit+predict), 25 km pan-Arctic day, fp64"
 X0 = np.array([np.log(25e3), np.log(25e3), 0.0, 0.0, 0.0, np.log(.1)])  # GPR:217
 X0_12P5 = np.array([np.log(12.5e3), np.log(12.5e3), 0.0, 0.0, 0.0, np.log(.1)])  # GPR:217, grid_res = 12.5
@@ -66,7 +67,7 @@ def parse():
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=2)
     p.add_argument('--workload', default='day',
-                   choices=['day', 'days', 'season', 'predict', 'single', 'nystrom', 'svgp'])
+                   choices=['day', 'days', 'season', 'predict', 'single', 'nystrom', 'svgp', 'twopass'])
     p.add_argument('--season-shares', type=int, default=8,
                    help='season workload: the 12.5 km day is LPT-split into this many GPU shares; rank r '
                         'fits share r (config 5 = 8 shares on 8 GPUs; at N = 1 one 1/8 share)')
@@ -210,7 +211,7 @@ def check_shares(args, world, shares):
         raise SystemExit(f"bench.py: --day-shares {args.day_shares} with {world} ranks would leave shares unfitted")
 
 
-def default_depth(args, world, nslices):
+def default_depth(args, world, nslices, per_day=None):
     """Slices in flight beyond the one waited on, keyed on the per-rank work
     (ADVICE r4), never on the GPU count alone:
       * a rank's SHARE of a day (config 4 at N > 1, --day-shares runs, and the
@@ -218,8 +219,13 @@ def default_depth(args, world, nslices):
         into its session at once, so the rounds stay near the 1-GPU resident
         size (8 shares at depth 20 on one GPU: 0.90 projected efficiency,
         profiles/r04/day_share_8of8.json);
+      * the season's depth is keyed on the slices of ONE day (``per_day``,
+        ADVICE r5), so consecutive days stream through the session instead of
+        all K days' inputs being submitted at once;
       * a WHOLE day per rank (config 3, and `days` at any N) keeps 8 slices
         in flight, as the headline always has."""
+    if args.workload == 'season' and per_day:
+        return max(1, int(max(per_day))), "the slices of one season day (a rank's share of that day)"
     share = args.workload == 'season' or (args.workload == 'day' and (world > 1 or args.day_shares))
     return (max(1, nslices), "every slice (a rank's share of a day)") if share else (8, "8 (a whole day per rank)")
 
@@ -395,7 +401,7 @@ def reference_evals_model():
     return E, desc, float(np.mean(bucket))
 
 
-def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline):
+def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline, extra_pred=0):
     """The CPU oracle (oracle/gp_oracle.py, bit-exact restatement of
     GPR_CS2S3.py:78-191 with scipy's CG) on this host's cores, one
     single-threaded-BLAS process per core:
@@ -450,7 +456,7 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline):
     except Exception as e:  # fixture missing: the sample fits' mean, flat in n
         e_cells = np.full(len(n), float(np.mean([f['evals'] for f in fits])))
         e_src, e_fix = f"the {len(fits)} sample fits' mean evaluation count, flat in n ({e!r})", None
-    t_cells = k * e_cells * t_eval(n) + t_pred(n)
+    t_cells = k * e_cells * t_eval(n) + (1 + extra_pred) * t_pred(n)  # extra_pred: pass 2 (GPR:316-319)
     value = len(n) / (float(np.sum(t_cells)) / workers)
     small = n <= 600
     return {"value": value, "unit": "grid-cells/s", "cores": workers, "kind": "port",
@@ -471,6 +477,7 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline):
             "fit_time_total_residual": round(float(np.sum(k * model) / np.sum(meas) - 1.0), 4),
             "fit_time_residuals": [round(float(r), 4) for r in resid],
             "probe_s": {str(kk): [round(v[0], 5), round(v[1], 5)] for kk, v in med.items()},
+            "t_eval_coef": [float(v) for v in ce], "t_pred_coef": [float(v) for v in cp],
             "cpu_s_per_cell_mean": round(float(np.mean(t_cells)), 3)}
 
 
@@ -743,6 +750,161 @@ def main_svgp(args, torch, dist, world, rank, gpu, cdev):
         dist.destroy_process_group()
 
 
+# ----------------------------------------------------------------- twopass
+TWOPASS_CHECK = r'''
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from scipy.spatial import cKDTree
+from oracle import day_oracle as D, gp_oracle as G
+d = np.load(sys.argv[2])
+sat, sie, x, y, mean, T, rad = d['sat'], d['sie'], d['x'], d['y'], float(d['mean']), int(d['T']), float(d['radius'])
+x_train, y_train, t_train, z = D.training_set(sat, x, y)
+IDs = np.where(~np.isnan(sie))
+X = np.array([x[IDs], y[IDs]]).T
+out = {}
+if sys.argv[3] == 'smooth':   # GPR:299-307 on the GPU's own pass-1 fields: bit-exact expected
+    same = []
+    for k, (key, vmax) in enumerate(zip(D.SMOOTH_VMAX_KEYS, D.smooth_vmax(rad, T))):
+        ref = D.smooth(d['p1'][k], vmax, sie, int(d['std']))
+        a = d['sm'][k]
+        same.append(bool(np.array_equal(np.isnan(a), np.isnan(ref)) and np.array_equal(a[~np.isnan(a)], ref[~np.isnan(ref)])))
+    out = {"smooth_bit_exact": same}
+else:                        # pass 2 (GPR:316-319 -> GPR3D opt=False, GPR:169-182) of sampled cells
+    tree = cKDTree(np.array([x_train, y_train]).T)
+    rel = lambda a, b: abs(a - b) / max(1.0, abs(b))
+    wf, ws, ns = 0.0, 0.0, []
+    for q, c in enumerate(d['cells']):
+        ID = tree.query_ball_point(x=X[c, :], r=rad * 1000)
+        inputs = np.array([x_train[ID], y_train[ID], t_train[ID]]).T
+        hyp = tuple(float(v) for v in d['hyp'][q])
+        fs, sd = G.gp_cell(inputs, z[ID], np.array([X[c, 0], X[c, 1], T // 2]), mean, opt=False, hyp=hyp)
+        wf, ws = max(wf, rel(d['fs'][q], fs)), max(ws, rel(d['sd'][q], sd))
+        ns.append(len(ID))
+    out = {"max_rel_fs": wf, "max_rel_sd": ws, "n": ns}
+print(json.dumps(out))
+'''
+
+
+def main_twopass(args, torch, dist, world, rank, gpu, cdev):
+    """The reference's WHOLE two-pass day (VERDICT r5 item 4): GPR_CS2S3.py
+    :223-246 training set, :159 radius query, :258-262 pass 1 (CG fit +
+    predict) and its exchange, :299-307 the five smoothings, :311 the
+    broadcast, :169-172 hyper lookup, :316-320 pass 2 and its gather -- the
+    production output `_interp_smth` -- as day.interpolate_day on a binned
+    synthetic 25 km day (synthetic.make_binned_day: ~1e4 ice cells, ~300-3000
+    observations within 300 km).  A step is one whole day (seed + step)."""
+    import tempfile
+    from optimalinterpolation_amd import _lib, day as DAY, synthetic
+    days = [synthetic.make_binned_day(seed=args.seed + k) for k in range(args.steps)]
+    if not args.no_prime:
+        w = synthetic.make_binned_day(seed=999, nx=40, ice_radius_m=110e3, obs_radius_m=450e3, cover=(0.02, 0.05))
+        DAY.interpolate_day(w.sat, w.sie, w.x, w.y, w.mean, date='w', rank=rank, world=world, device=gpu,
+                            comm_device=cdev)
+    _lib.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = []
+    for k, d in enumerate(days):
+        res.append(DAY.interpolate_day(d.sat, d.sie, d.x, d.y, d.mean, date=d.date, rank=rank, world=world,
+                                       device=gpu, comm_device=cdev, profile=True))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    prof = _lib.profile_json()
+    r0, d0 = res[0], days[0]
+    ids = np.where(~np.isnan(d0.sie))
+    ncell = int(sum(r.info['ncell'] for r in res))
+    tim = {k: round(float(np.sum([r.info['timing'][k] for r in res])), 3)
+           for k in ('neighbours_s', 'pass1_s', 'smooth_s', 'pass2_s', 'total_s')}
+    evals = np.concatenate([np.asarray(r.info['evals'], float) for r in res])
+    counts = np.concatenate([np.asarray(r.info['counts'], float) for r in res])
+    # distinct sites per cell (the m x m problem the library solves), host-side for the flop model
+    from scipy.spatial import cKDTree
+    sites = []
+    for d in days:
+        xt, yt, tt_, _ = DAY.training_set(d.sat, d.x, d.y)
+        idd = np.where(~np.isnan(d.sie))
+        tree = cKDTree(np.column_stack([xt, yt]))
+        key = np.column_stack([xt, yt, tt_]).view(np.dtype((np.void, 24))).ravel()
+        for lst in tree.query_ball_point(np.column_stack([d.x[idd], d.y[idd]]), r=synthetic.RADIUS_M):
+            sites.append(len(np.unique(key[np.asarray(lst, dtype=np.int64)])))
+    n = np.asarray(sites, float)
+    ok = np.isfinite(evals)
+    rl = roofline_of(prof, np.where(ok, evals, 0.0), n, dt, counts, extra_pred=1)
+    line = {"metric": "grid-cells/sec (whole two-pass day: fit+predict, smooth, predict), 25 km, fp64",
+            "value": round(ncell / dt, 4), "unit": "grid-cells/s", "n_gpus": world, "steps": args.steps,
+            "warmup": 0, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic binned day (synthetic.make_binned_day: 320x320 grid, 4 satellites x 9 days)",
+            "config": {"workload": ("the reference's whole day GPR_CS2S3.py:223-336 per step: training set, "
+                                    "300 km query, pass 1 CG fit + predict, all-gather, 5 smoothings, hyper lookup, "
+                                    "pass 2 predict (the production `_interp_smth`), gather; binned grids on the "
+                                    "host, the training set assembled and uploaded inside the timed region"),
+                       "day_cells": int(r0.info['ncell']), "n_train": int(r0.info['n_train']),
+                       "obs_per_cell_mean": round(float(np.mean(counts)), 1),
+                       "obs_per_cell_range": [int(counts.min()), int(counts.max())],
+                       "parallelism": f"dp{world} (LPT cell partition; one all_gather after pass 1, one gather "
+                                      f"after pass 2)"},
+            "stages_s": tim, "pass2_share": round(tim['pass2_s'] / max(tim['total_s'], 1e-12), 5),
+            "pass2_cells_per_s": round(ncell / max(tim['pass2_s'], 1e-12), 1),
+            "evals_per_cell": round(float(np.mean(evals[ok])), 2), "failed_cells": int(np.sum(~ok)),
+            "roofline": rl, **args.dist_fields}
+    # parity: smoothing bit-exact on the GPU's own pass-1 fields; pass 2 of sampled cells at T1
+    tmp = tempfile.mkdtemp(prefix='oi_twopass_')
+    path = os.path.join(tmp, 'day.npz')
+    p1 = np.stack([r0[d0.date + '_' + k] for k in DAY.HYPER_KEYS])
+    sm = np.stack([r0[d0.date + '_' + k + '_smth'] for k in DAY.HYPER_KEYS])
+    order = np.argsort(counts[:len(ids[0])], kind='stable')
+    pick = np.array([int(b[len(b) // 2]) for b in np.array_split(order, max(1, args.parity_cells)) if len(b)])
+    np.savez(path, sat=d0.sat, sie=d0.sie, x=d0.x, y=d0.y, mean=d0.mean, T=synthetic.T_DAYS, radius=300.0,
+             std=DAY.smooth_std(25), p1=p1, sm=sm, cells=pick,
+             hyp=np.column_stack([s_[ids][pick] for s_ in sm]),
+             fs=r0[d0.date + '_interp_smth'][ids][pick], sd=r0[d0.date + '_interp_error_smth'][ids][pick])
+    deadline = time.time() + 600
+    chk = run_argv_jobs(TWOPASS_CHECK, [[path, 'smooth']] +
+                        [[path, 'pass2']], 2, deadline)
+    par = {"cells": int(len(pick)), "tol": 1e-10}
+    if chk[0] is not None:
+        par["smooth_bit_exact"] = chk[0]["smooth_bit_exact"]
+    if chk[1] is not None:
+        par.update(max_rel_fs=chk[1]["max_rel_fs"], max_rel_sd=chk[1]["max_rel_sd"],
+                   n_min=min(chk[1]["n"]), n_max=max(chk[1]["n"]))
+    par["pass"] = bool(chk[0] is not None and chk[1] is not None and all(par["smooth_bit_exact"])
+                       and par["max_rel_fs"] <= 1e-10 and par["max_rel_sd"] <= 1e-10)
+    par["note"] = ("day 0: the oracle's smoothing (GPR:65-76 restated) of the GPU's pass-1 fields vs the GPU's "
+                   "smoothed fields (bitwise), and the oracle's GPR3D(opt=False) with the reference's cKDTree "
+                   "neighbour order at the GPU's smoothed hypers vs the GPU's pass-2 fs / sd on a stratified "
+                   "sample of cells (T1)")
+    line["parity"] = par
+    if world == 1 and not args.no_cpu_baseline:
+        workers, desc = host_cores(args)
+        try:
+            line["cpu_baseline"] = cpu_baseline(counts[ok], evals[ok], workers, desc, time.time() + 400,
+                                                extra_pred=1)
+        except Exception as e:
+            line["cpu_baseline"] = {"value": None, "error": repr(e)}
+    else:
+        line["cpu_baseline"] = None
+    s = json.dumps(line)
+    print(s, flush=True)
+    if args.out:
+        with open(args.out, 'w') as f:
+            f.write(s + '\n')
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------- launcher
 def visible_gpus():
     """GPUs a rank process will see, counted in a child process: the launcher
@@ -763,7 +925,7 @@ def free_port():
         return so.getsockname()[1]
 
 
-def launch_ranks(n, argv, script=None, gpus=None, backend=None, grace_s=20.0, poll_s=0.25):
+def launch_ranks(n, argv, script=None, gpus=None, backend=None, grace_s=20.0, poll_s=0.25, deadline_s=None):
     """`bench.py --gpus N` without a launcher around it: start N rank
     processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
     MASTER_PORT in their environment, the torch.distributed.run contract),
@@ -773,7 +935,9 @@ def launch_ranks(n, argv, script=None, gpus=None, backend=None, grace_s=20.0, po
     ``grace_s``) and its code is returned.  Called before this process imports
     anything that touches the GPU; ranks are started as children, never by
     exec.  ``gpus``: visible GPU count (probed in a child when None); N > gpus
-    is refused (exit 2) unless the backend is gloo."""
+    is refused (exit 2) unless the backend is gloo.  ``deadline_s`` (seconds
+    from T_PROC): ranks still running then -- e.g. one stuck in a
+    collective after another exited 0 -- are ended and 124 is returned."""
     import signal
     import threading
     backend = backend or os.environ.get('OI_DIST_BACKEND', 'nccl')
@@ -823,6 +987,12 @@ def launch_ranks(n, argv, script=None, gpus=None, backend=None, grace_s=20.0, po
                 log(f"rank {procs.index(bad[0])} exited with {rc}: ending the other ranks")
                 end_all()
                 break
+            if deadline_s is not None and elapsed() > deadline_s:
+                live = [r for r, p in enumerate(procs) if p.poll() is None]
+                log(f"launcher deadline {deadline_s:.0f} s passed with ranks {live} still running: ending them")
+                end_all()
+                rc = 124
+                break
             time.sleep(poll_s)
     finally:
         signal.signal(signal.SIGTERM, prev)
@@ -869,6 +1039,18 @@ def heartbeat(period=60.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
+def per_rank_record(rank, cells, dt, outs, done_k, opt, tprof):
+    """[rank, cells fitted, own timed seconds, SMLII evaluations, GPU ms of the
+    rounds with < 256 resident cells (-1 without per-launch profiling)]."""
+    from optimalinterpolation_amd import _lib
+    ev = float(sum(float(np.sum(outs[k][2][:, 3])) for k in range(done_k))) if opt else 0.0
+    tail = -1.0
+    if tprof:
+        rl = _lib.profile_json().get('rounds_log') or []
+        tail = float(sum(r[4] for r in rl if r[0] + r[1] < 256))
+    return [rank, float(cells), float(dt), ev, tail]
+
+
 def site_counts(cells):
     """Distinct (x, y, t) sites per cell: the size of the problem the library
     solves (oi_device.h "Duplicate sites"); host-side, for the flop model."""
@@ -876,7 +1058,7 @@ def site_counts(cells):
     return np.array([len(np.unique(v[a:b])) for a, b in zip(cells.offs[:-1], cells.offs[1:])], dtype=np.int64)
 
 
-def roofline_of(prof, evals, n, dt, n_obs=None):
+def roofline_of(prof, evals, n, dt, n_obs=None, extra_pred=0):
     """Roofline of the dominant kernel from the library's HIP-event profile
     (every launch of the timed region, on the stream the kernels run on).
     ``n``: the solved size per cell (distinct sites); ``n_obs``: observations
@@ -891,7 +1073,7 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
     # trtri = 2n^3/3 per evaluation and potrf n^3/3 per predict, k_lauum_grad
     # the lauum n^3/3 per evaluation; each kernel gets its family's algorithmic
     # flops in proportion to its share of the family's executed tile products.
-    fam_alg = {'factor': float(np.sum((evals * 2.0 / 3.0 + 1.0 / 3.0) * n ** 3)),
+    fam_alg = {'factor': float(np.sum((evals * 2.0 / 3.0 + (1.0 + extra_pred) / 3.0) * n ** 3)),
                'lauum': float(np.sum(evals * n ** 3 / 3.0))}
     fam_of = {'k_panel_even': 'factor', 'k_panel4': 'factor', 'k_chol_panel': 'factor',
               'k_lauum_grad': 'lauum'}
@@ -924,9 +1106,10 @@ def roofline_of(prof, evals, n, dt, n_obs=None):
             traffic = json.load(open(tfile)).get(dom, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    useful = float(np.sum(evals * (n ** 3 + 40 * n ** 2) + n ** 3 / 3 + 16 * n ** 2))
+    npred = 1 + extra_pred  # predict blocks per cell (pass 2 of the two-pass day adds one)
+    useful = float(np.sum(evals * (n ** 3 + 40 * n ** 2) + npred * (n ** 3 / 3 + 16 * n ** 2)))
     no = n if n_obs is None else n_obs
-    ref_eq = float(np.sum(evals * (no ** 3 + 40 * no ** 2) + no ** 3 / 3 + 16 * no ** 2))
+    ref_eq = float(np.sum(evals * (no ** 3 + 40 * no ** 2) + npred * (no ** 3 / 3 + 16 * no ** 2)))
     return {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
             "traffic_note": ("HBM bytes per launch of this kernel, rocprofv3 PMC FETCH_SIZE(x2, gfx950)+WRITE_SIZE, "
@@ -959,7 +1142,8 @@ def main():
     args = parse()
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
         # no launcher around us: start the ranks ourselves, before any GPU call
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        # deadline: the slice budget + the rank-0 parity check / teardown
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], deadline_s=args.budget_s + LAUNCH_GRACE_S))
     heartbeat()
     # one resident-cell group (one stream): OI_GROUPS=2 overlaps one group's
     # latency-bound launches with the other's GEMMs, +0.5 % on the day
@@ -983,7 +1167,10 @@ def main():
         raise SystemExit(f"bench.py: LOCAL_RANK {local} but {ndev} GPU(s) visible: refusing to put two "
                          f"ranks on one GPU (OI_DIST_BACKEND=gloo for a one-GPU rehearsal)")
     gpu = local % max(1, ndev)
-    per_dev = -(-world // max(1, ndev))  # ranks sharing one GPU (the gloo rehearsal)
+    # ranks sharing one GPU (the gloo rehearsal): this node's ranks, not the
+    # global world (2 nodes x 8 GPUs must not halve every arena)
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', '') or world)
+    per_dev = -(-local_world // max(1, ndev))
     if per_dev > 1:  # each rank's library arena takes a share of the HBM, not 60 % of what is left
         os.environ.setdefault('OI_ARENA_FRAC', f"{0.8 / per_dev:.4f}")
     # the rank's device is current before the process group exists, so RCCL's
@@ -1005,11 +1192,13 @@ def main():
         return main_nystrom(args, torch, dist, world, rank, gpu, cdev)
     if args.workload == 'svgp':
         return main_svgp(args, torch, dist, world, rank, gpu, cdev)
+    if args.workload == 'twopass':
+        return main_twopass(args, torch, dist, world, rank, gpu, cdev)
     from optimalinterpolation_amd import _lib, synthetic
 
     slices, warm, opt, cfg, scaling, counts_all = build_slices(args, rank, world)
     if args.depth is None:
-        args.depth, cfg["depth_rule"] = default_depth(args, world, len(slices))
+        args.depth, cfg["depth_rule"] = default_depth(args, world, len(slices), cfg.get("slices_per_day"))
     cfg["depth"] = args.depth
     x0 = X0_12P5 if args.workload == 'season' else X0
     log(f"rank {rank}: {len(slices)} slices, {sum(s.ncell for s in slices)} cells")
@@ -1110,11 +1299,19 @@ def main():
     dt = time.perf_counter() - t0
     if sess is not None:
         sess.close()
+    ncells_rank = sum(slices[k].ncell for k in range(done_k))
+    # per-rank evidence (GPR:256,262's scatter/gather): every
+    # rank's cells, own timed seconds, SMLII evaluations and the GPU time of its
+    # tail rounds (< 256 resident cells), so the scaling line shows imbalance
+    per_rank = [per_rank_record(rank, ncells_rank, dt, outs, done_k, opt, tprof)]
     if world > 1:
+        mine = torch.tensor(per_rank[0][1:], dtype=torch.float64, device=cdev)
+        allr = [torch.zeros(4, dtype=torch.float64, device=cdev) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [[r] + [float(v) for v in t.tolist()] for r, t in enumerate(allr)]
         tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    ncells_rank = sum(slices[k].ncell for k in range(done_k))
     tot = torch.tensor([float(ncells_rank)], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot)
@@ -1152,6 +1349,10 @@ def main():
             "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
             "failed_cells": int(np.sum(status != 0)), "timed_s": round(dt, 3),
             "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float)), **args.dist_fields}
+    line["per_rank"] = [{"rank": int(r), "cells": int(c), "timed_s": round(t, 3), "evals": int(e),
+                         "tail_round_gpu_ms": (round(m, 1) if m >= 0 else None)} for r, c, t, e, m in per_rank]
+    if world > 1:
+        line["config"]["cells_per_rank"] = [int(c) for c in counts_all]
     if not tprof:
         line["roofline"]["timing_note"] = ("per-launch HIP-event times from a second, profiled pass over the "
                                            "same cells; the timed pass runs without per-launch events")

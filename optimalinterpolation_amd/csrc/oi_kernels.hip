@@ -374,6 +374,11 @@ __device__ __forceinline__ void trtri4w(double* As, double* dump) {
 
 // LDS of the diagonal factor: As (packed L / Inv) | Vs | sites (j = 0) | bad
 #define DIAG_LDS (NB * DW_LD + 3 * NB + 4 * NB + 2)
+// diag_tile(j + 1) runs inside the panel kernels on their GEMM LDS arrays
+// (the fused look-ahead factor, oi_engine.cpp OI_FUSE_DIAG_MIN)
+static_assert(DIAG_LDS <= GEMM1_LDS, "the diagonal factor must fit k_chol_panel's LDS");
+static_assert(DIAG_LDS <= GEMM2_LDS, "the diagonal factor must fit k_panel_even's LDS");
+static_assert(DIAG_LDS <= GEMM4_LDS, "the diagonal factor must fit k_panel4's LDS");
 
 // the body of k_diag_factor4w for cell c and tile j: 256 threads work, any
 // larger workgroup passes every barrier with them; `lds` holds DIAG_LDS doubles

@@ -584,7 +584,7 @@ struct Lane {
 // batched Cholesky per group, (5) the triangular solve, objective and
 // prediction of every cell.
 // Per-cell phases are dealt round-robin over LANES (OI_NYS_LANES, default 1:
-// stream + rocBLAS handle + scratch each; more lanes measured no faster with
+// stream + oila::gemm descriptor ring + scratch each; more lanes measured no faster with
 // the box's 4 hardware queues); per-slot state (scaled inputs,
 // K_mm -> u, s, st, C, B -> L) lives in chunk-sized slot arrays.
 class Runner {
@@ -1015,8 +1015,8 @@ class Runner {
         KCHK();
         sg.end();
       } else {
-        // Ki = Vi - W'W (full GEMM: rocBLAS dsyrk at this shape is ~2x slower than
-        // dgemm although it does half the flops; the sweep below reads the lower half)
+        // Ki = Vi - W'W (OI_NYS_FUSED=0 only: one full oila::gemm product; the
+        // sweep below reads the lower half)
         sg.begin(S_KI, 2.0 * dn * dn * dM, 8.0 * dn * dn);
         oila::gemm(L.la, st, false, true, {oila::Gemm{Wt, Wt, Ki, R.in, R.in, R.iM, R.in, R.in, R.in, -1.0, 0.0, 0}});
         hipLaunchKernelGGL(k_nys_diag, dim3(blocks(R.n, 256)), dim3(256), 0, st, Ki, R.n, R.n, nullptr,

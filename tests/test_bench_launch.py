@@ -28,6 +28,10 @@ RANK_SCRIPT = textwrap.dedent('''
         time.sleep(120)          # the launcher must end this rank
     if mode == "noline":
         sys.exit(0)
+    if mode == "stuck0":         # rank 1 exits 0, rank 0 hangs (e.g. in a collective)
+        if r == 1:
+            sys.exit(0)
+        time.sleep(120)
     if mode == "dist":
         import torch, torch.distributed as dist
         dist.init_process_group("gloo")
@@ -74,6 +78,15 @@ def test_failing_rank_ends_the_others_and_sets_the_exit_code(rank_script):
     assert time.time() - t0 < 60          # rank 0 / 2 (sleeping 120 s) were ended, not waited for
 
 
+def test_launcher_deadline_ends_a_stuck_rank(rank_script):
+    """a rank stuck after another exited 0 is ended at the deadline."""
+    t0 = time.time()
+    rc = bench.launch_ranks(2, ['stuck0'], script=rank_script, gpus=8, backend='nccl', grace_s=5.0,
+                            deadline_s=bench.elapsed() + 8.0)
+    assert rc == 124
+    assert time.time() - t0 < 60
+
+
 def test_rank0_without_a_line_is_a_failure(rank_script):
     assert bench.launch_ranks(2, ['noline'], script=rank_script, gpus=8, backend='nccl') == 1
 
@@ -118,3 +131,5 @@ def test_default_depth_depends_on_the_per_rank_work_not_the_gpu_count():
     assert bench.default_depth(_args(workload='day'), 1, 20)[0] == 8
     assert bench.default_depth(_args(workload='day', day_shares=8), 1, 20)[0] == 20
     assert bench.default_depth(_args(workload='day'), 8, 20)[0] == 20
+    # the season: keyed on one day's slices, not every slice of K days
+    assert bench.default_depth(_args(workload='season'), 1, 60, [20, 20, 20])[0] == 20

@@ -141,6 +141,11 @@ def test_bench_self_launch_gloo(tmp_path):
     assert line['config']['cells_total'] == 96 and line['failed_cells'] == 0
     assert line['steps'] == 4 and not line.get('truncated')
     assert line['parity']['pass'], line['parity']
+    # per-rank evidence: both ranks, their cells summing to the day
+    pr = line['per_rank']
+    assert [r['rank'] for r in pr] == [0, 1] and sum(r['cells'] for r in pr) == 96
+    assert line['config']['cells_per_rank'] == [r['cells'] for r in pr]
+    assert all(r['timed_s'] > 0 and r['evals'] > 0 for r in pr)
 
 
 def test_bench_under_torchrun_gloo(tmp_path):

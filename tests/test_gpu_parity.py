@@ -342,6 +342,35 @@ def test_panel4_equals_panel_even(monkeypatch):
         assert np.array_equal(a, b), np.max(np.abs(a - b) / np.maximum(1, np.abs(b)))
 
 
+def test_fused_diag_factor_equals_separate_launches(monkeypatch):
+    """The look-ahead workgroup of column j's panel launch factors diagonal
+    tile j+1 (default, OI_FUSE_DIAG_MIN=1); with OI_FUSE_DIAG_MIN above the
+    round size every column's diagonal tile is factored by its own
+    k_diag_factor4w launch instead.  Same arithmetic on the same
+    LDS layout: objective, gradient, predictions and a full fit bitwise equal,
+    for both even-column kernels."""
+    sizes = [1, 63, 64, 65, 129, 192, 257, 700, 1100, 2000]
+    cells = synthetic.make_cells(sizes, seed=29)
+    h = np.tile(np.array([np.log(2e5), np.log(2.5e5), np.log(7.), np.log(4e-3), np.log(1e-3), 0.]), (len(sizes), 1))
+    mX = np.full(len(cells.z), cells.mean)
+    hyp = np.tile(synthetic.FIXED_HYPERS, (len(sizes), 1))
+    fit = synthetic.make_cells([300, 700], seed=31)
+    monkeypatch.setenv('OI_PANEL4_MINT', '0')
+    monkeypatch.setenv('OI_PANEL4_MINWG', '0')
+    res = {}
+    for p4 in ('0', '1'):
+        for fuse in ('1', '100000'):
+            monkeypatch.setenv('OI_PANEL4', p4)
+            monkeypatch.setenv('OI_FUSE_DIAG_MIN', fuse)
+            ev = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, h)
+            pr = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
+            ft = _lib.gpr_batch(fit.xyt, fit.z, fit.offs, fit.xs, fit.mean, opt=True, info=True)
+            res[(p4, fuse)] = (ev[0], ev[1], pr[0][:, :3], ft[0], ft[2][:, 3])
+    for p4 in ('0', '1'):
+        for a, b in zip(res[(p4, '1')], res[(p4, '100000')]):
+            assert np.array_equal(a, b, equal_nan=True), (p4, a, b)
+
+
 def test_cell_result_independent_of_round_mates(monkeypatch):
     """A cell's results never depend on the other cells of its rounds: small
     cells (T < 12, k_panel_even when alone) fitted and evaluated alone, and
