@@ -61,11 +61,6 @@ typedef double dv2 __attribute__((ext_vector_type(2)));
 // next chunks, exposing HBM latency once per chunk.
 typedef __attribute__((address_space(1))) const dv2 gdv2;
 __device__ __forceinline__ dv2 gload2(const double* p) { return *(gdv2*)p; }
-// non-temporal (`nt`) form for operands one workgroup streams once
-__device__ __forceinline__ dv2 gload2_nt(const double* p) { return __builtin_nontemporal_load((gdv2*)p); }
-#ifndef OI_NT_A
-#define OI_NT_A 0  // gemm4_kmajor: A operands (private to the workgroup) loaded nt
-#endif
 struct StageRegs {
   dv2 a0, a1, b0, b1;
 };
@@ -288,13 +283,8 @@ __device__ __forceinline__ void gemm4_kmajor(Quad8& acc, double* lds, int nch, u
     const double *pa0, *pa1, *pb0, *pb1;
     [[clang::always_inline]] pair(ch >> 2, pa0, pa1, pb0, pb1);
     const int off = (ch & 3) * KC * GNB + t * 2;
-#if OI_NT_A
-    q.a0 = gload2_nt(pa0 + off);
-    q.a1 = gload2_nt(pa1 + off);
-#else
     q.a0 = gload2(pa0 + off);
     q.a1 = gload2(pa1 + off);
-#endif
     q.b0 = gload2(pb0 + off);
     q.b1 = gload2(pb1 + off);
   };

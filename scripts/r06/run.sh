@@ -27,6 +27,7 @@
 #   twopass         bench.py --workload twopass (the whole two-pass day, GPR:223-336)
 #   cpu-model       scripts/r06/cpu_model_check.py (host only: the CPU-baseline model at n = 1500..3000)
 #   pmc-tcc         TCC hit / miss / fabric-read counters of the day's kernels ($OI_LIB if set)
+#   day-abn         the day over the builds in $LIBS ("cur" = the tree), round robin, $REPS rounds
 # Profiles of the driver's command: scripts/r05/gpu_prof.sh; end-of-round
 # verification: scripts/r05/gpu_verify.sh.
 set -o pipefail
@@ -111,6 +112,15 @@ for step in "$@"; do
       rc=$?; echo "tcc rc $rc"; [ $rc -eq 0 ] || { tail -5 $D/pmcT.err; exit $rc; }
       python3 scripts/pmc_kernels.py $D/pmcT > $D/pmc_tcc${OI_LIB:+_$(basename $OI_LIB .so)}.txt && rm -rf $D/pmcT
       cut -c1-260 $D/pmc_tcc*.txt | head -8 ;;
+    day-abn)  # the day over the builds in $LIBS ("cur" = the tree's liboi.so), round robin, ${REPS:-2} rounds
+      fail=0; k=0
+      for rep in $(seq ${REPS:-2}); do for lib in $LIBS; do
+        k=$((k + 1)); E=""; [ $lib != cur ] && E="OI_LIB=$lib"; tag=$(basename $lib .so)
+        env $E timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --parity-cells 8 \
+          --out $D/day_${tag}_$k.json > $D/day_${tag}_$k.log 2>&1 || { tail -20 $D/day_${tag}_$k.log; fail=1; break 2; }
+        show $D/day_${tag}_$k.json "$tag"
+        python3 -c "import json,sys; r=json.load(open(sys.argv[1]))['roofline']; print('   ', {k: round(v / 1e3, 3) for k, v in r['kernels_ms'].items() if v > 100})" $D/day_${tag}_$k.json
+      done; done; [ $fail = 0 ] ;;
     *) echo "unknown step $step"; false ;;
   esac || { echo "step $step failed"; exit 1; }
 done

@@ -364,7 +364,8 @@ def test_fused_diag_factor_equals_separate_launches(monkeypatch):
             monkeypatch.setenv('OI_FUSE_DIAG_MIN', fuse)
             ev = _lib.nlml_grad_batch(cells.xyt, cells.z, mX, cells.offs, h)
             pr = _lib.gpr_batch(cells.xyt, cells.z, cells.offs, cells.xs, cells.mean, opt=False, hyp=hyp)
-            ft = _lib.gpr_batch(fit.xyt, fit.z, fit.offs, fit.xs, fit.mean, opt=True, info=True)
+            ft = _lib.gpr_batch(fit.xyt, fit.z, fit.offs, fit.xs, fit.mean, opt=True, info=True,
+                                x0=np.array([np.log(25e3), np.log(25e3), 0., 0., 0., np.log(.1)]))
             res[(p4, fuse)] = (ev[0], ev[1], pr[0][:, :3], ft[0], ft[2][:, 3])
     for p4 in ('0', '1'):
         for a, b in zip(res[(p4, '1')], res[(p4, '100000')]):
