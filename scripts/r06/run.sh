@@ -28,6 +28,7 @@
 #   cpu-model       scripts/r06/cpu_model_check.py (host only: the CPU-baseline model at n = 1500..3000)
 #   pmc-tcc         TCC hit / miss / fabric-read counters of the day's kernels ($OI_LIB if set)
 #   day-abn         the day over the builds in $LIBS ("cur" = the tree), round robin, $REPS rounds
+#   config1-trace   rocprofv3 kernel trace of config 1: per-kernel durations and the gaps between launches
 # Profiles of the driver's command: scripts/r05/gpu_prof.sh; end-of-round
 # verification: scripts/r05/gpu_verify.sh.
 set -o pipefail
@@ -121,6 +122,11 @@ for step in "$@"; do
         show $D/day_${tag}_$k.json "$tag"
         python3 -c "import json,sys; r=json.load(open(sys.argv[1]))['roofline']; print('   ', {k: round(v / 1e3, 3) for k, v in r['kernels_ms'].items() if v > 100})" $D/day_${tag}_$k.json
       done; done; [ $fail = 0 ] ;;
+    config1-trace)  # kernel durations and inter-kernel gaps of config 1 (one n = 200 cell per step)
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $D/c1t -o run --output-format csv -- python3 bench.py --workload single \
+        --steps 10 --warmup 2 --no-cpu-baseline --timed-profile off > $D/config1_trace.json 2> $D/config1_trace.err
+      rc=$?; [ $rc -eq 0 ] || { tail -5 $D/config1_trace.err; exit $rc; }
+      python3 scripts/trace_summary.py $D/c1t > $D/config1_trace_summary.txt && rm -rf $D/c1t && cat $D/config1_trace_summary.txt ;;
     *) echo "unknown step $step"; false ;;
   esac || { echo "step $step failed"; exit 1; }
 done
