@@ -346,6 +346,8 @@ else:
 
 EVAL_PROBES = (300, 600, 1000, 1500, 2000, 2500, 3000)
 FIT_SAMPLE = tuple(range(300, 601, 20))   # 16 cells, stratified over n in [300, 600]
+FIT_LARGE = (2000, 2000, 1500, 1500)      # k at large n (k from small fits alone over-predicted
+                                          # n = 1500..3000 fits by 4-16 %, profiles/r06/cpu_model_check.json)
 
 
 def run_jobs(jobs, workers, deadline):
@@ -409,17 +411,22 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline, extra_pred=0):
         n = 300..3000 (the second of two calls in the process), 3 repetitions
         each (median), all timed while ``workers`` processes run at once,
         fitted t = a + b n^2 + c n^3 by relative least squares;
-      * k: the ratio measured / modelled time of 16 full oracle GPR3D(opt=True)
-        fits at n = 300..600 run on the same host, each modelled as its own
-        evaluation count x t_eval(n) + t_pred(n) (k absorbs the optimiser's
-        Python per evaluation); the residual of every fit after k is reported;
+      * k(n): the ratio measured / modelled time of full oracle GPR3D(opt=True)
+        fits run on the same host, each modelled as its own evaluation count x
+        t_eval(n) + t_pred(n) (k absorbs the optimiser's Python per evaluation,
+        which matters at small n): the median over 16 fits at n = 300..600
+        (k_small) and over 4 fits at n = 1500..2000 (k_large), interpolated in
+        log t_eval(n) between the two groups' median sizes and held constant
+        outside them; the residual of every fit after k(n) is reported;
       * E(n): the reference's own evaluations per cell on this day's cells
         (reference_evals_model: tests/golden/day_ref_fits.npz), not the GPU's;
-      * value = cells / (sum over the timed cells of k E(n) t_eval(n) + t_pred(n))
+      * value = cells / (sum over the timed cells of k(n) E(n) t_eval(n) + t_pred(n))
         x workers -- extrapolated, labelled so."""
     t0 = time.time()
     jobs = [('eval', n, 11 * n + r) for n in sorted(EVAL_PROBES, reverse=True) for r in range(3)]
-    jobs = jobs[:6] + [('fit', n, 13 * n + 1) for n in FIT_SAMPLE] + jobs[6:]
+    # the large fits first (each runs ~0.5-2 minutes), then the probes and the small fits
+    jobs = ([('fit', n, 13 * n + 1 + r) for r, n in enumerate(FIT_LARGE)] + jobs[:6]
+            + [('fit', n, 13 * n + 1) for n in FIT_SAMPLE] + jobs[6:])
     res = run_jobs(jobs, workers, deadline)
     ev = [r for r in res if r['kind'] == 'eval']
     fits = [r for r in res if r['kind'] == 'fit']
@@ -448,23 +455,37 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline, extra_pred=0):
     gpu_evals = np.asarray(gpu_evals, float)
     model = np.array([f['evals'] * t_eval(f['n']) + t_pred(f['n']) for f in fits])
     meas = np.array([f['fit_s'] for f in fits])
-    k = float(np.median(meas / model))
-    resid = meas / (k * model) - 1.0
+    fn = np.array([f['n'] for f in fits], float)
+    sm_f, lg_f = fn <= 600, fn > 600
+    k_s = float(np.median((meas / model)[sm_f])) if sm_f.any() else float(np.median(meas / model))
+    k_l = float(np.median((meas / model)[lg_f])) if lg_f.any() else k_s
+    n_s = float(np.median(fn[sm_f])) if sm_f.any() else 450.0
+    n_l = float(np.median(fn[lg_f])) if lg_f.any() else n_s
+
+    def k_of(nn):  # linear in log t_eval between the two calibration groups, constant outside
+        x = np.log(t_eval(np.asarray(nn, float)))
+        xs, xl = np.log(t_eval(n_s)), np.log(t_eval(n_l))
+        w = np.clip((x - xs) / (xl - xs), 0.0, 1.0) if xl > xs else np.zeros_like(x)
+        return k_s + w * (k_l - k_s)
+    k = float(k_of(np.median(sizes))) if len(sizes) else k_s
+    resid = meas / (k_of(fn) * model) - 1.0
     try:
         E, e_src, e_fix = reference_evals_model()
         e_cells = E(n)
     except Exception as e:  # fixture missing: the sample fits' mean, flat in n
         e_cells = np.full(len(n), float(np.mean([f['evals'] for f in fits])))
         e_src, e_fix = f"the {len(fits)} sample fits' mean evaluation count, flat in n ({e!r})", None
-    t_cells = k * e_cells * t_eval(n) + (1 + extra_pred) * t_pred(n)  # extra_pred: pass 2 (GPR:316-319)
+    t_cells = k_of(n) * e_cells * t_eval(n) + (1 + extra_pred) * t_pred(n)  # extra_pred: pass 2 (GPR:316-319)
     value = len(n) / (float(np.sum(t_cells)) / workers)
     small = n <= 600
     return {"value": value, "unit": "grid-cells/s", "cores": workers, "kind": "port",
             "sample": (f"oracle/gp_oracle.py (bit-exact restatement of GPR_CS2S3.py:78-191 + scipy CG) on "
                        f"{workers} single-threaded-BLAS processes ({cores_desc}); measured: one SMLII eval + "
                        f"one predict at n={ns} x3 reps (median, fitted a+bn^2+cn^3, relative least squares) and "
-                       f"{len(fits)} full GPR3D(opt=True) fits at n=300..600 (measured / modelled time "
-                       f"k = {k:.3f}, residuals after k {np.min(resid):+.3f} .. {np.max(resid):+.3f}); "
+                       f"{int(sm_f.sum())} full GPR3D(opt=True) fits at n=300..600 and {int(lg_f.sum())} at "
+                       f"n=1500..2000 (measured / modelled time k = {k_s:.3f} at n={n_s:.0f}, {k_l:.3f} at "
+                       f"n={n_l:.0f}, interpolated in log t_eval; residuals after k(n) {np.min(resid):+.3f} .. "
+                       f"{np.max(resid):+.3f}); "
                        f"extrapolated to the {len(n)} timed cells with E(n) = {e_src} "
                        f"({time.time() - t0:.0f} s wall): extrapolated"),
             "e_cpu_mean_timed_cells": round(float(np.mean(e_cells)), 2),
@@ -473,6 +494,9 @@ def cpu_baseline(sizes, gpu_evals, workers, cores_desc, deadline, extra_pred=0):
             "e_cpu_sample_fits": round(float(np.mean([f['evals'] for f in fits])), 2),
             "e_gpu_small": round(float(np.mean(gpu_evals[small])), 2) if small.any() else None,
             "fit_time_model_k": round(k, 4),
+            "fit_time_model_k_small_large": [round(k_s, 4), round(k_l, 4)],
+            "fit_time_model_k_anchor_n": [n_s, n_l],
+            "fit_sizes": [int(v) for v in fn],
             "fit_time_residual_max_abs": round(float(np.max(np.abs(resid))), 4),
             "fit_time_total_residual": round(float(np.sum(k * model) / np.sum(meas) - 1.0), 4),
             "fit_time_residuals": [round(float(r), 4) for r in resid],

@@ -424,3 +424,56 @@ def test_profile_by_j_matches_kernel_totals():
     jp = sorted({r[1] for r in byj if r[0] in ('k_panel4', 'k_panel_even', 'k_chol_panel')})
     assert jp == list(range(len(jp))) and len(jp) >= 2
 
+
+
+# Hyper-parameter points the chaotic CG does reach (line searches
+# overshoot into overflow -- cell 37 of the day fixture made 111 inf
+# evaluations, DESIGN §2b history): length-scales and variances far outside
+# the data's range, exp() over- and underflowing (GPR:120-122).  The class of
+# the result must be the reference's exactly -- NaN where numpy's cholesky
+# propagates NaN (GPR:126 raises only for a non-positive finite pivot), inf
+# where it raises LinAlgError (GPR:139-140) -- because scipy's line search
+# branches on it; finite values at the T1 tolerance.
+EXTREME_H = {
+    'huge_ell': [30, 30, 30, 0, 0, 0],
+    'tiny_ell': [-30, -30, -30, 0, -5, 0],
+    'big_sf2': [12, 12, 1, 50, 0, 0],
+    'tiny_sn2': [12, 12, 1, 0, -50, 0],
+    'ell_overflow': [800, 12, 1, 0, 0, 0],
+    'sf2_overflow': [12, 12, 1, 800, 0, 0],
+    'sn2_overflow': [12, 12, 1, 0, 800, 0],
+    'sn2_underflow': [12, 12, 1, 0, -800, 0],
+    'ell_underflow': [-800, 12, 1, 0, 0, 0],
+    'nan_h': [np.nan, 12, 1, 0, 0, 0],
+}
+
+
+@pytest.mark.parametrize('dedup', ['1', '0'])
+def test_extreme_hypers_match_reference_class(dedup, monkeypatch):
+    monkeypatch.setenv('OI_DEDUP', dedup)
+    cells = synthetic.make_cells([50, 300, 700], seed=77)
+    names = list(EXTREME_H)
+    h = np.array([EXTREME_H[k] for k in names for _ in range(cells.ncell)], float)
+    big = synthetic.RaggedCells(np.concatenate([cells.xyt] * len(names)), np.concatenate([cells.z] * len(names)),
+                                np.concatenate([[0]] + [cells.offs[1:] + k * cells.offs[-1] for k in range(len(names))]),
+                                np.concatenate([cells.xs] * len(names)), cells.mean)
+    mX = np.full(len(big.z), cells.mean)
+    nlz, grad, st = _lib.nlml_grad_batch(big.xyt, big.z, mX, big.offs, h)
+    bad = []
+    with np.errstate(all='ignore'):
+        for q in range(big.ncell):
+            x, y, _ = big.cell(q)
+            f, g = O.neg_log_ml(h[q], x, y, np.full(len(y), cells.mean))
+            f = float(np.asarray(f).ravel()[0])
+            name, n = names[q // cells.ncell], len(y)
+            cls = lambda v: 'nan' if np.isnan(v) else ('+inf' if v == np.inf else '-inf' if v == -np.inf else 'fin')
+            if cls(nlz[q]) != cls(f) or [cls(v) for v in grad[q, :5]] != [cls(v) for v in np.asarray(g)[:5]]:
+                bad.append((name, n, 'class', nlz[q], f, grad[q, :5].tolist(), np.asarray(g)[:5].tolist()))
+                continue
+            if np.isfinite(f):
+                ok, err = close(nlz[q], f)
+                sc = np.abs(g) + grad_scale(h[q], x, y, np.full(len(y), cells.mean))
+                okg, errg = close(grad[q], g, scale=np.maximum(sc, 1e-300))
+                if not (ok and okg):
+                    bad.append((name, n, 'value', err, errg))
+    assert not bad, bad
