@@ -466,8 +466,11 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds) {
     // sf2 + sn2 rounds to sf2, sn2 = 0 included; with probability 1/2 at
     // sn2 / sf2 = OI_DUP_NONPD_TAU n_obs) and takes the LinAlgError branch
     // (GPR:139-140); the m x m site form would not notice (oi_device.h).
+    // (a non-finite sf2 -- exp overflow at a CG trial point -- makes the
+    // reference's K inf / NaN, which numpy's cholesky propagates as NaN rather
+    // than raising: no not-PD flag then, the NaNs run through as they do there)
     const double sf2 = c.hyp[3], sn2 = c.hyp[4];
-    if (c.n_obs > c.n && (sf2 + sn2 == sf2 || sn2 < OI_DUP_NONPD_TAU * c.n_obs * sf2)) {
+    if (c.n_obs > c.n && isfinite(sf2) && (sf2 + sn2 == sf2 || sn2 < OI_DUP_NONPD_TAU * c.n_obs * sf2)) {
       if (t == 0) *c.status = OI_NOT_PD;
       return;
     }
@@ -1560,7 +1563,13 @@ __device__ __forceinline__ void finalize_cell(const OiCell& c) {
       const double sf2 = c.hyp[3], sn2 = c.hyp[4], nm = (double)(c.n_obs - c.n);
       c.out[0] = c.mean + p[1];
       c.out[1] = sqrt(sf2 - p[2]);
-      c.out[2] = ((-(p[0] + c.ssw / sn2)) / 2 - (p[3] + (nm / 2) * log(sn2))) - (c.n_obs * LOG2PI) / 2;
+      // the duplicate-site terms only where sites repeat (nm > 0): without
+      // repeats they are exact zeros, and at sn2 = 0 (exp underflow, GPR:122)
+      // 0 / 0 and 0 * log 0 would turn the reference's finite lZ into NaN
+      if (nm > 0.0)
+        c.out[2] = ((-(p[0] + c.ssw / sn2)) / 2 - (p[3] + (nm / 2) * log(sn2))) - (c.n_obs * LOG2PI) / 2;
+      else
+        c.out[2] = ((-p[0]) / 2 - p[3]) - (c.n_obs * LOG2PI) / 2;
     }
     return;
   }
@@ -1593,12 +1602,19 @@ __device__ __forceinline__ void finalize_cell(const OiCell& c) {
     // sum log diag L = log det M / 2 + (n - m)/2 log sn2, tr Q += (n - m)/sn2 - SSW/sn2^2
     const double quad = v[5], logdet = v[6], sn2 = c.hyp[4];
     const double nm = (double)(c.n_obs - c.n);
-    c.out[0] = ((quad + c.ssw / sn2) / 2 + (logdet + (nm / 2) * log(sn2))) + (c.n_obs * LOG2PI) / 2;
+    // (n - m) and SSW terms only where sites repeat: without repeats they are
+    // exact zeros, and at sn2 = 0 (exp underflow of the CG's trial point,
+    // GPR:122) 0 / 0 and 0 * log 0 would give NaN where the reference's nlZ and
+    // sn2 tr Q (= 0) are finite
+    if (nm > 0.0)
+      c.out[0] = ((quad + c.ssw / sn2) / 2 + (logdet + (nm / 2) * log(sn2))) + (c.n_obs * LOG2PI) / 2;
+    else
+      c.out[0] = (quad / 2 + logdet) + (c.n_obs * LOG2PI) / 2;
     c.out[1] = v[0] / 2;
     c.out[2] = v[1] / 2;
     c.out[3] = v[2] / 2;
     c.out[4] = v[3] / 2;
-    c.out[5] = sn2 * ((v[4] + nm / sn2) - c.ssw / (sn2 * sn2));
+    c.out[5] = nm > 0.0 ? sn2 * ((v[4] + nm / sn2) - c.ssw / (sn2 * sn2)) : sn2 * v[4];
     c.out[6] = 0.0;
   }
 }

@@ -433,7 +433,11 @@ def test_profile_by_j_matches_kernel_totals():
 # the result must be the reference's exactly -- NaN where numpy's cholesky
 # propagates NaN (GPR:126 raises only for a non-positive finite pivot), inf
 # where it raises LinAlgError (GPR:139-140) -- because scipy's line search
-# branches on it; finite values at the T1 tolerance.
+# branches on it; finite values at the T1 tolerance.  (Round 6: this test
+# found two class mismatches, both fixed -- sn2 = exp(-800) = 0 gave NaN
+# through the duplicate-site terms' 0/0 where the reference is finite, and an
+# infinite sf2 tripped the duplicate not-PD rule where numpy's cholesky
+# propagates NaN.)
 EXTREME_H = {
     'huge_ell': [30, 30, 30, 0, 0, 0],
     'tiny_ell': [-30, -30, -30, 0, -5, 0],
@@ -445,6 +449,12 @@ EXTREME_H = {
     'sn2_underflow': [12, 12, 1, 0, -800, 0],
     'ell_underflow': [-800, 12, 1, 0, 0, 0],
     'nan_h': [np.nan, 12, 1, 0, 0, 0],
+    'sf2_underflow': [12, 12, 1, -800, 0, 0],
+    'lt_overflow': [12, 12, 800, 0, 0, 0],
+    'all_overflow': [800, 800, 800, 800, 800, 0],
+    'sf2_huge_sn2_tiny': [12, 12, 1, 300, -300, 0],
+    'neg_inf_h': [-np.inf, 12, 1, 0, 0, 0],
+    'pos_inf_sn2': [12, 12, 1, 0, np.inf, 0],
 }
 
 
