@@ -85,3 +85,44 @@ def test_inf_objective_paths():
     for a, b in zip(req, calls):
         assert np.array_equal(a, b)
     assert np.array_equal(mine['x'], res.x) and mine['status'] == res.status
+
+
+def _scipy_vs_restatement(fun, x0):
+    import scipy.optimize
+    calls = []
+
+    def rec(h):
+        calls.append(np.array(h).copy())
+        return fun(h)
+    with np.errstate(all='ignore'):
+        res = scipy.optimize.minimize(rec, x0=x0, method='CG', jac=True)
+    req, mine = drive(np.array(x0, float), lambda h, k: fun(h))
+    assert len(req) == len(calls)
+    for a, b in zip(req, calls):
+        assert np.array_equal(a, b)
+    assert np.array_equal(mine['x'], res.x, equal_nan=True)
+    assert mine['status'] == res.status and mine['nit'] == res.nit and mine['nfev'] == res.nfev
+    return res
+
+
+@pytest.mark.parametrize('radius', [3.0, 1.5, 0.2])
+def test_nan_objective_paths(radius):
+    """Objective = NaN (nlZ and gradient) beyond a radius: the reference's value
+    where exp over- / underflows at a trial point makes K inf / NaN and numpy's
+    cholesky propagates it (GPR:120-126; the GPU path returns the same class,
+    tests/test_gpu_parity.py::test_extreme_hypers_match_reference_class) --
+    scipy's CG then stops with status 3 ("NaN result encountered") or backs
+    off; the restatement must follow it step for step."""
+    c = np.array([1, -2, 0.5, 2.9, -1, 0])
+
+    def fun(h):
+        if np.abs(h).max() > radius:
+            return np.nan, np.full(6, np.nan)
+        return float(np.sum((h - c) ** 2 * np.arange(1, 7))), 2 * (h - c) * np.arange(1, 7)
+    _scipy_vs_restatement(fun, np.zeros(6))
+
+
+def test_nan_objective_at_x0():
+    """A NaN objective at the starting point (every entry of x0 overflowing):
+    scipy's outcome, exactly."""
+    _scipy_vs_restatement(lambda h: (np.nan, np.full(6, np.nan)), np.zeros(6))
