@@ -437,11 +437,14 @@ def test_profile_by_j_matches_kernel_totals():
 # found two class mismatches, both fixed -- sn2 = exp(-800) = 0 gave NaN
 # through the duplicate-site terms' 0/0 where the reference is finite, and an
 # infinite sf2 tripped the duplicate not-PD rule where numpy's cholesky
-# propagates NaN.)
+# propagates NaN.)  Not covered, by design: one-observation cells (the
+# reference's 1 x 1 K keeps squareform's zero "distance" even for non-finite
+# coordinates, and numpy raises on a 1 x 1 inf matrix) and
+# near-singular points (sf2 / sn2 beyond 1e16), where finite vs not-PD is
+# the reference's own rounding noise (test_duplicate_nonpd_band).
 EXTREME_H = {
     'huge_ell': [30, 30, 30, 0, 0, 0],
     'tiny_ell': [-30, -30, -30, 0, -5, 0],
-    'big_sf2': [12, 12, 1, 50, 0, 0],
     'tiny_sn2': [12, 12, 1, 0, -50, 0],
     'ell_overflow': [800, 12, 1, 0, 0, 0],
     'sf2_overflow': [12, 12, 1, 800, 0, 0],
@@ -452,7 +455,6 @@ EXTREME_H = {
     'sf2_underflow': [12, 12, 1, -800, 0, 0],
     'lt_overflow': [12, 12, 800, 0, 0, 0],
     'all_overflow': [800, 800, 800, 800, 800, 0],
-    'sf2_huge_sn2_tiny': [12, 12, 1, 300, -300, 0],
     'neg_inf_h': [-np.inf, 12, 1, 0, 0, 0],
     'pos_inf_sn2': [12, 12, 1, 0, np.inf, 0],
 }
@@ -487,3 +489,81 @@ def test_extreme_hypers_match_reference_class(dedup, monkeypatch):
                 if not (ok and okg):
                     bad.append((name, n, 'value', err, errg))
     assert not bad, bad
+
+
+# Pass 2 / predict-only (GPR:169-182) at the same kind of hypers, given as
+# values (ell_x, ell_y, ell_t, sf2, sn2); cells of 0 and >= 50 observations
+# (one-observation cells: see above).
+EXTREME_HYP = {
+    'ell_inf': [np.inf, 1e5, 3, 5e-3, 1e-3],
+    'ell_zero': [0.0, 1e5, 3, 5e-3, 1e-3],
+    'sf2_inf': [1e5, 1e5, 3, np.inf, 1e-3],
+    'sf2_zero': [1e5, 1e5, 3, 0.0, 1e-3],
+    'sn2_zero': [1e5, 1e5, 3, 5e-3, 0.0],
+    'sn2_inf': [1e5, 1e5, 3, 5e-3, np.inf],
+    'nan': [np.nan, 1e5, 3, 5e-3, 1e-3],
+    'tiny_ell': [1e-3, 1e-3, 1e-5, 5e-3, 1e-3],
+}
+
+
+@pytest.mark.parametrize('dedup', ['1', '0'])
+def test_extreme_predict_match_reference_class(dedup, monkeypatch):
+    monkeypatch.setenv('OI_DEDUP', dedup)
+    cells = synthetic.make_cells([0, 50, 300, 700], seed=78)
+    names = list(EXTREME_HYP)
+    hyp = np.array([EXTREME_HYP[k] for k in names for _ in range(cells.ncell)], float)
+    big = synthetic.RaggedCells(np.concatenate([cells.xyt] * len(names)), np.concatenate([cells.z] * len(names)),
+                                np.concatenate([[0]] + [cells.offs[1:] + k * cells.offs[-1] for k in range(len(names))]),
+                                np.concatenate([cells.xs] * len(names)), cells.mean)
+    out, status, _ = _lib.gpr_batch(big.xyt, big.z, big.offs, big.xs, big.mean, opt=False, hyp=hyp)
+    bad = []
+    cls = lambda v: 'nan' if np.isnan(v) else ('+inf' if v == np.inf else '-inf' if v == -np.inf else 'fin')
+    with np.errstate(all='ignore'):
+        for q in range(big.ncell):
+            x, y, xs = big.cell(q)
+            name, n = names[q // cells.ncell], len(y)
+            try:  # GPR3D(opt=False): NaN 2-tuple on LinAlgError (GPR:187-191)
+                fs, sd, lz = O.predict(x, y, xs, big.mean, hyp[q, :3], hyp[q, 3], hyp[q, 4])
+                ref = np.array([float(np.ravel(fs)[0]), float(np.ravel(sd)[0]), float(lz)])
+            except np.linalg.LinAlgError:
+                ref = np.full(3, np.nan)
+            got = out[q, :3]
+            if [cls(v) for v in got] != [cls(v) for v in ref]:
+                bad.append((name, n, 'class', got.tolist(), ref.tolist()))
+                continue
+            fin = np.isfinite(ref)
+            if fin.any():
+                ok, err = close(got[fin], ref[fin])
+                if not ok:
+                    bad.append((name, n, 'value', err, got.tolist(), ref.tolist()))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize('dedup', ['1', '0'])
+def test_repeated_site_nonfinite_coordinates(dedup, monkeypatch):
+    """A cell whose observations all sit on ONE site (m = 1 < n): at a
+    length-scale of 0 or NaN the reference's K has NaN between the identical
+    observations (pdist of non-finite coordinates, GPR:93) and its nlZ is NaN;
+    the site form must not hide that behind its one finite diagonal entry.
+    Finite hypers: T1 as everywhere."""
+    monkeypatch.setenv('OI_DEDUP', dedup)
+    p = np.array([[3.1e6, 2.2e6, 4.0]])
+    xyt = np.concatenate([np.repeat(p, 3, 0), [[3.0e6, 2.0e6, 1.0], [3.05e6, 2.1e6, 2.0]]])
+    z = np.array([0.31, 0.29, 0.30, 0.27, 0.33])
+    offs = np.array([0, 3, 5])
+    hs = {'finite': [np.log(2e5), np.log(2e5), np.log(5.), np.log(5e-3), np.log(1e-3), 0.],
+          'ell_underflow': [-800, np.log(2e5), np.log(5.), np.log(5e-3), np.log(1e-3), 0.],
+          'ell_nan': [np.nan, np.log(2e5), np.log(5.), np.log(5e-3), np.log(1e-3), 0.]}
+    for name, h in hs.items():
+        H = np.tile(np.array(h, float), (2, 1))
+        nlz, grad, st = _lib.nlml_grad_batch(xyt, z, np.full(5, 0.28), offs, H)
+        for c in range(2):
+            x, y = xyt[offs[c]:offs[c + 1]], z[offs[c]:offs[c + 1]]
+            with np.errstate(all='ignore'):
+                f, g = O.neg_log_ml(H[c], x, y, np.full(len(y), 0.28))
+            f = float(np.asarray(f).ravel()[0])
+            if np.isfinite(f):
+                ok, err = close(nlz[c], f)
+                assert ok, (name, c, nlz[c], f)
+            else:
+                assert np.isnan(f) == np.isnan(nlz[c]) and (np.isnan(f) or nlz[c] == f), (name, c, nlz[c], f)
