@@ -1305,6 +1305,7 @@ def main():
     for k in range(done_k):
         if k not in outs:
             outs[k] = sess.wait(tickets[k])
+    t_own = time.perf_counter() - t0  # this rank's own work done (before the gather and the closing barrier)
     # the single gather of posterior fields (ncell x 8 fp64) to rank 0
     rows = np.concatenate([outs[k][0] for k in range(done_k)]) if done_k else np.zeros((0, 8))
     if world > 1:
@@ -1325,9 +1326,11 @@ def main():
         sess.close()
     ncells_rank = sum(slices[k].ncell for k in range(done_k))
     # per-rank evidence (GPR:256,262's scatter/gather): every
-    # rank's cells, own timed seconds, SMLII evaluations and the GPU time of its
-    # tail rounds (< 256 resident cells), so the scaling line shows imbalance
-    per_rank = [per_rank_record(rank, ncells_rank, dt, outs, done_k, opt, tprof)]
+    # rank's cells, the seconds until its own last slice was done (the timed
+    # region itself ends at a common barrier), SMLII evaluations and the GPU
+    # time of its tail rounds (< 256 resident cells), so the scaling line shows
+    # imbalance
+    per_rank = [per_rank_record(rank, ncells_rank, t_own, outs, done_k, opt, tprof)]
     if world > 1:
         mine = torch.tensor(per_rank[0][1:], dtype=torch.float64, device=cdev)
         allr = [torch.zeros(4, dtype=torch.float64, device=cdev) for _ in range(world)]
@@ -1373,7 +1376,7 @@ def main():
             "config": cfg, "evals_per_cell": round(float(np.mean(evals)), 2) if opt else 0,
             "failed_cells": int(np.sum(status != 0)), "timed_s": round(dt, 3),
             "roofline": roofline_of(prof, evals, n, dt, sizes_timed.astype(float)), **args.dist_fields}
-    line["per_rank"] = [{"rank": int(r), "cells": int(c), "timed_s": round(t, 3), "evals": int(e),
+    line["per_rank"] = [{"rank": int(r), "cells": int(c), "own_work_s": round(t, 3), "evals": int(e),
                          "tail_round_gpu_ms": (round(m, 1) if m >= 0 else None)} for r, c, t, e, m in per_rank]
     if world > 1:
         line["config"]["cells_per_rank"] = [int(c) for c in counts_all]
