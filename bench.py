@@ -111,6 +111,8 @@ def parse():
     p.add_argument('--parity-cells', type=int, default=24,
                    help='day workloads: timed cells re-checked against the CPU oracle at the GPU fit\'s '
                         'hypers (T1, SURVEY §8c), stratified over n; 0 = skip')
+    p.add_argument('--twopass-small', action='store_true',
+                   help='twopass workload: a small binned day (48 x 48 grid, ~100 cells) -- tests / rehearsals only')
     p.add_argument('--dump', default='', help='write per-cell n, m, evals, status of the timed cells (.npz)')
     p.add_argument('--out', default='')
     return p.parse_args()
@@ -820,7 +822,8 @@ def main_twopass(args, torch, dist, world, rank, gpu, cdev):
     observations within 300 km).  A step is one whole day (seed + step)."""
     import tempfile
     from optimalinterpolation_amd import _lib, day as DAY, synthetic
-    days = [synthetic.make_binned_day(seed=args.seed + k) for k in range(args.steps)]
+    small = dict(nx=48, ice_radius_m=200e3, obs_radius_m=500e3, cover=(0.02, 0.06)) if args.twopass_small else {}
+    days = [synthetic.make_binned_day(seed=args.seed + k, **small) for k in range(args.steps)]
     if not args.no_prime:
         w = synthetic.make_binned_day(seed=999, nx=40, ice_radius_m=110e3, obs_radius_m=450e3, cover=(0.02, 0.05))
         DAY.interpolate_day(w.sat, w.sie, w.x, w.y, w.mean, date='w', rank=rank, world=world, device=gpu,
@@ -862,7 +865,7 @@ def main_twopass(args, torch, dist, world, rank, gpu, cdev):
         tree = cKDTree(np.column_stack([xt, yt]))
         key = np.column_stack([xt, yt, tt_]).view(np.dtype((np.void, 24))).ravel()
         for lst in tree.query_ball_point(np.column_stack([d.x[idd], d.y[idd]]), r=synthetic.RADIUS_M):
-            sites.append(len(np.unique(key[np.asarray(lst, dtype=np.int64)])))
+            sites.append(max(1, len(np.unique(key[np.asarray(lst, dtype=np.int64)]))))
     n = np.asarray(sites, float)
     ok = np.isfinite(evals)
     rl = roofline_of(prof, np.where(ok, evals, 0.0), n, dt, counts, extra_pred=1)

@@ -175,3 +175,25 @@ def test_bench_under_torchrun_gloo(tmp_path):
     assert line['config']['cells_total'] == 96 and line['failed_cells'] == 0
     assert line['steps'] == 4 and not line.get('truncated')
     assert line['parity']['pass'], line['parity']
+
+
+def test_bench_twopass_small(tmp_path):
+    """`bench.py --workload twopass` (the reference's whole two-pass day,
+    GPR:223-336) end to end on a small binned day: the line's parity block
+    (smoothing bit-exact vs the oracle on the GPU's own pass-1 fields, pass-2
+    cells at T1) passes and the stages add up."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / 'twopass.json'
+    p = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--workload', 'twopass', '--twopass-small',
+                        '--steps', '1', '--no-cpu-baseline', '--parity-cells', '6', '--out', str(out)],
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(out.read_text())
+    assert line['parity']['pass'], line['parity']
+    assert all(line['parity']['smooth_bit_exact'])
+    st = line['stages_s']
+    assert st['pass1_s'] > 0 and st['pass2_s'] > 0 and st['total_s'] >= st['pass1_s'] + st['pass2_s']
+    assert line['failed_cells'] == 0 and line['config']['day_cells'] > 20
