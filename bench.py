@@ -378,8 +378,8 @@ def run_jobs(jobs, workers, deadline):
 def reference_evals_model():
     """E(n): the REFERENCE's own SMLII evaluations per GPR3D(opt=True) fit.
 
-    Source: tests/golden/day_ref_fits.npz -- GPR_CS2S3.py:143-191 run on 232
-    cells of the bench day itself (synthetic.make_day(seed=0)) in 5
+    Source: tests/golden/day_ref_fits.npz -- GPR_CS2S3.py:143-191 run on the
+    fixture's cells of the bench day itself (synthetic.make_day(seed=0)) in 5
     observation orders each (tests/golden/make_day_fits.py): the mean over the
     fixture's cells and runs in each 300-wide n bucket from 300 to 3000.  Above
     n = 3000 (config 5) the reference's fits of n = 2500..5000 in

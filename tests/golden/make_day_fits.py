@@ -4,7 +4,7 @@
 times (VERDICT r3 "next round" item 1).
 
 Run in the build container only (it reads /root/reference):
-    python tests/golden/make_day_fits.py [--jobs 7] [--partial]
+    python tests/golden/make_day_fits.py [--jobs 7] [--partial] [--extend]
 
 Cells (seeded selection, written into the fixture as day indices):
   * strata: 8 cells in every 300-wide n bucket 300-600, ..., 2700-3000
@@ -53,6 +53,8 @@ PER_STRATUM = 8
 N_SMALL = 160
 LARGE_STRATA = tuple(range(600, 3000, 300))
 LARGE_PER_STRATUM = 16
+EXTRA_CELLS = 320        # round 6 (--extend): more cells with 300 <= n < 1200, drawn from their own seed
+EXTRA_NMAX = 1200
 RADIUS_KM = 325                          # >= 300 km + the lattice's half diagonal (17.7 km)
 
 
@@ -81,6 +83,18 @@ def select_cells(sizes):
         chosen += pick.tolist()
         strat += [2] * LARGE_PER_STRATUM
     return np.array(chosen, dtype=np.int64), np.array(strat, dtype=np.int8)
+
+
+def select_extra(sizes, chosen):
+    """Round 6: EXTRA_CELLS further cells with n < EXTRA_NMAX (stratum flag 3),
+    from their own seed, none of them already in the fixture -- more samples
+    for the fleet rules, at a CPU cost (an n = 1200 fit is ~30 s) that lets
+    every cell keep its 5 reference orders."""
+    import numpy as np
+    rng = np.random.default_rng(SELECT_SEED + 2)
+    pool = np.setdiff1d(np.flatnonzero(sizes < EXTRA_NMAX), chosen)
+    pick = np.sort(rng.choice(pool, EXTRA_CELLS, replace=False))
+    return pick.astype(np.int64), np.full(EXTRA_CELLS, 3, dtype=np.int8)
 
 
 _DAY = {}
@@ -152,9 +166,17 @@ def main():
     ap.add_argument('--partial', action='store_true',
                     help='write the fixture from the cells whose runs are all cached; run nothing new')
     ap.add_argument('--only-small', action='store_true', help='run the n < 600 cells only (dry runs)')
+    ap.add_argument('--extend', action='store_true',
+                    help='round 6: keep the fixture at --out as it is and append the EXTRA_CELLS cells '
+                         '(select_extra), fitting only those')
     args = ap.parse_args()
     d = day()
     cells, strat = select_cells(d.sizes)
+    old = None
+    if args.extend:
+        old = dict(np.load(args.out))
+        assert np.array_equal(old['cells'], cells), "the fixture is not the select_cells one"
+        cells, strat = select_extra(d.sizes, cells)
     if args.only_small:
         keep = d.sizes[cells] < 600
         cells, strat = cells[keep], strat[keep]
@@ -186,9 +208,14 @@ def main():
         nlz.append(nlz_all[ci * NRUNS:(ci + 1) * NRUNS])
     IX, offs = ragged(inx, 3)
     IY, _ = ragged(iny, 1)
-    np.savez_compressed(args.out, x=IX, y=IY, offs=offs, xs=d.xs[cells], cells=cells, stratum=strat,
-                        sizes=d.sizes[cells], mean=d.mean, out8=np.array(out8), evals=np.array(evals),
-                        nlz=np.array(nlz), sec=np.array(secs), day_seed=DAY_SEED, radius_km=RADIUS_KM,
+    arr = dict(x=IX, y=IY, offs=offs, xs=d.xs[cells], cells=cells, stratum=strat, sizes=d.sizes[cells],
+               out8=np.array(out8), evals=np.array(evals), nlz=np.array(nlz), sec=np.array(secs))
+    if old is not None:  # append to the existing fixture (its arrays untouched)
+        arr['offs'] = np.concatenate([old['offs'], old['offs'][-1] + arr['offs'][1:]])
+        for k in ('x', 'y', 'xs', 'cells', 'stratum', 'sizes', 'out8', 'evals', 'nlz', 'sec'):
+            arr[k] = np.concatenate([old[k], arr[k]])
+        cells = arr['cells']
+    np.savez_compressed(args.out, **arr, mean=d.mean, day_seed=DAY_SEED, radius_km=RADIUS_KM,
                         numpy=np.__version__, scipy=scipy.__version__, ref=REF, lines=f'{FIRST}-{LAST}')
     print(f"wrote {args.out}: {len(cells)} cells", flush=True)
 

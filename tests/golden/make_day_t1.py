@@ -16,7 +16,7 @@ observations, run r > 0 permuted by default_rng(7000 + 13 idx + r), then the
 reference's cKDTree query at 325 km, GPR:159-161); order 0 is asserted equal
 to the fixture's stored inputs.  Writes day_ref_t1.npz (numeric arrays
 only).  Build container only (reads /root/reference):
-    python tests/golden/make_day_t1.py [--jobs 7]
+    python tests/golden/make_day_t1.py [--jobs 7] [--extend]
 """
 import argparse
 import os
@@ -86,13 +86,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--jobs', type=int, default=7)
     ap.add_argument('--out', default=os.path.join(HERE, 'day_ref_t1.npz'))
+    ap.add_argument('--extend', action='store_true',
+                    help='keep the cells already in --out and compute only the cells day_ref_fits.npz added since')
     args = ap.parse_args()
     fx, _ = state()
     sizes = fx['sizes']
-    jobs = sorted([(k, r) for k in range(len(sizes)) for r in range(NRUNS)], key=lambda j: -int(sizes[j[0]]))
+    k0 = 0
+    if args.extend:
+        old = dict(np.load(args.out))
+        k0 = len(old['cells'])
+        assert np.array_equal(old['cells'], fx['cells'][:k0]), "day_ref_t1.npz is not a prefix of day_ref_fits.npz"
+    jobs = sorted([(k, r) for k in range(k0, len(sizes)) for r in range(NRUNS)], key=lambda j: -int(sizes[j[0]]))
     nlz = np.full((len(sizes), 2, NRUNS), np.nan)
     grad = np.full((len(sizes), 2, NRUNS, 6), np.nan)
     hyp = np.full((len(sizes), 2, 6), np.nan)
+    if args.extend:
+        nlz[:k0], grad[:k0], hyp[:k0] = old['nlz'], old['grad'], old['hyp']
     with Pool(args.jobs) as pool:
         for i, (k, r, res, pts) in enumerate(pool.imap_unordered(job, jobs)):
             nlz[k, :, r] = res[:, 0]

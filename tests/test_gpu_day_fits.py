@@ -1,5 +1,5 @@
 """T3 on the HEADLINE's own cells: the
-GPU's GPR3D(opt=True) fits of 360 cells of the bench day itself
+GPU's GPR3D(opt=True) fits of 680 cells of the bench day itself
 (``synthetic.make_day(seed=0)``, the day `bench.py` times) against the
 REFERENCE's own fits of the same cells (tests/golden/day_ref_fits.npz, made by
 tests/golden/make_day_fits.py running GPR_CS2S3.py:143-191 -- CG at :166 --
@@ -8,10 +8,13 @@ on each cell's observations in 5 orders: run 0 as drawn, runs 1-4 permuted).
 Cells: 8 in every 300-wide n bucket from 300 to 3000 (72), 160 more with
 n < 600 (the day's smallest bucket) for the distribution of the evaluation
 count, and (round 5) 16 more in every bucket from 600 to 3000 (128), so that
-n >= 600 holds 192 cells.  Both site forms are fitted: ``OI_DEDUP=1`` (the default, the m x m
+n >= 600 holds 192 cells -- the 360 cells the rules below were set on --
+and (round 6) a replication sample of 320 further cells with n < 1200 drawn
+from their own seed (stratum 3), judged separately by the statistical tests
+alone (test_day_fits_replication_sample).  Both site forms are fitted: ``OI_DEDUP=1`` (the default, the m x m
 duplicate-site form) and ``OI_DEDUP=0`` (the plain n x n form).
 
-Rules (360 samples, no slack cells), each also as a statistical test of the
+Rules (on the 360 cells, no slack cells), each also as a statistical test of the
 hypothesis they stand for -- the GPU fit is one more observation order of
 the reference -- since two noisy counts over the same cells are
 not ordered by an unbiased fit:
@@ -68,6 +71,21 @@ def fits(dedup):
     return _CACHE[dedup]
 
 
+def base_cells(d):
+    """The cells the literal rules were set on (rounds 4-5: strata 0-2, 360
+    cells); round 6 appended a replication sample (stratum 3, 320 cells with
+    n < 1200) that is judged by the exchangeability tests alone
+    (test_day_fits_replication_sample)."""
+    return d['stratum'] != 3
+
+
+def sub(d, out, status, info, nlz_gpu, st, m):
+    """The fixture and the GPU's arrays restricted to the cells of mask m."""
+    dd = {k: d[k][m] for k in ('sizes', 'out8', 'nlz', 'evals', 'stratum')}
+    dd['offs'] = None
+    return dd, out[m], status[m], info[m], nlz_gpu[m], st[m]
+
+
 def test_fixture_is_the_bench_day():
     """The fixture's cells are cells of synthetic.make_day(seed=0) (the bench
     day): same sizes, targets and observations (run 0 holds them in the
@@ -93,9 +111,12 @@ def test_fixture_is_the_bench_day():
         assert np.sum(d['sizes'] >= 600) >= 190
 
 
-def _envelope(dedup):
+def _envelope(dedup, sample='base'):
     d, out, status, info, nlz_gpu, st = fits(dedup)
-    out8, nlz, sizes = d['out8'], d['nlz'], d['sizes']
+    m = base_cells(d) if sample == 'base' else ~base_cells(d)
+    idx = np.flatnonzero(m)
+    out8, nlz, sizes = d['out8'][m], d['nlz'][m], d['sizes'][m]
+    out, status, info, nlz_gpu, st = out[m], status[m], info[m], nlz_gpu[m], st[m]
     # a non-finite result is allowed only as scipy's own outcome: CG status 3
     # ("NaN result encountered", the restated scipy 1.15.3 of csrc/cg.cpp)
     bad = np.flatnonzero(((status != 0) | ~np.isfinite(out).all(1) | (st != 0)) & (info[:, 1] != 3))
@@ -107,7 +128,7 @@ def _envelope(dedup):
         tol = 1e-8 * abs(nlz[c, 0]) + 1e-9
         same = np.allclose(out[c], out8[c, 0], rtol=1e-6, atol=0)
         if not same and sizes[c] <= 1200 and len(checked) < 12 and np.isfinite(out[c]).all():
-            a, b = d['offs'][c], d['offs'][c + 1]
+            a, b = d['offs'][idx[c]], d['offs'][idx[c] + 1]
             xx, yy = d['x'].reshape(-1, 3)[a:b], d['y'][a:b]
             h = np.r_[np.log(out[c, 3:8]), np.log(.1)]
             f_cpu, _ = O.neg_log_ml(h, xx, yy, np.full(len(yy), float(d['mean'])))
@@ -118,7 +139,7 @@ def _envelope(dedup):
         if nlz[c, 4] > f_env + tol:
             miss_ref.append(c)
     k, expect, pval = worst_test(nlz_gpu, nlz)
-    print(f"OI_DEDUP={dedup}: GPU outside the reference's 4-run envelope in {len(miss)} of {len(sizes)} cells, "
+    print(f"OI_DEDUP={dedup} [{sample}]: GPU outside the reference's 4-run envelope in {len(miss)} of {len(sizes)} cells, "
           f"held-out reference run 4 in {len(miss_ref)}; GPU nlZ checked against the CPU oracle on "
           f"{len(checked)} cells; GPU the strict worst of 6 fits in {k} cells (expected {expect:.1f} if "
           f"exchangeable with the reference's orders, P(>= {k}) = {pval:.3f})")
@@ -183,7 +204,7 @@ def test_day_fits_fleet_rules(dedup):
     fraction beyond 1e-6 <= the reference's mean permuted fraction + its
     binomial standard error over the fixture's cells (the four permuted
     reference runs alone spanned 0.086 .. 0.099 on round 4's 232 cells)."""
-    d, out, status, info, nlz_gpu, st = fits(dedup)
+    d, out, status, info, nlz_gpu, st = sub(*fits(dedup), base_cells(fits(dedup)[0]))
     ref_fs = d['out8'][:, 0, 0]
     ok = np.isfinite(out[:, 0])
     rel = np.where(ok, np.abs(out[:, 0] - ref_fs) / np.abs(ref_fs), np.inf)
@@ -234,7 +255,7 @@ def test_day_fits_evaluation_ratio(dedup):
     contain 1; on round 5's 360 cells that CI is [1.0005, 1.019] (ratio 1.009)
     while the rank test gives z = 0.71 -- the ratio of sums is carried by a
     few cells' long CG runs, not by a shift."""
-    d, out, status, info, nlz_gpu, st = fits(dedup)
+    d, out, status, info, nlz_gpu, st = sub(*fits(dedup), base_cells(fits(dedup)[0]))
     ev, sizes = d['evals'].astype(float), d['sizes']
     lines = []
     for name, m in (('all', np.ones(len(sizes), bool)), ('n<600', sizes < 600), ('n>=600', sizes >= 600)):
@@ -260,7 +281,37 @@ def test_day_fits_evaluation_ratio_literal_ci():
     """The round-4 literal work rule (kept beside the rank test):
     the bootstrap 95 % CI of the GPU / reference evaluation ratio over all
     cells contains 1 for the default site form.  XPASS / XFAIL both recorded."""
-    d, out, status, info, nlz_gpu, st = fits(1)
+    d, out, status, info, nlz_gpu, st = sub(*fits(1), base_cells(fits(1)[0]))
     r, lo, hi = eval_ratio(info[:, 3], d['evals'].astype(float).mean(1))
     print(f"literal CI rule: ratio {r:.4f} [95 % CI {lo:.4f} .. {hi:.4f}]")
     assert lo <= 1.0 <= hi, (r, lo, hi)
+
+
+@pytest.mark.parametrize('dedup', [1, 0])
+def test_day_fits_replication_sample(dedup):
+    """Round 6: 320 further cells of the bench day with
+    n < 1200 (stratum 3, `make_day_fits.py --extend`), fitted by the
+    reference in 5 orders each, as an independent replication sample.  Judged
+    by the exchangeability tests the literal rules stand for (1 % level,
+    one-sided): the GPU the strict worst of the six fits no more often than a
+    random position would be (worst_test), its beyond-1e-6 indicator a random
+    one of the five orders' (order_test), its evaluation count ranking
+    uniformly among them (|z| < 2.58); the literal counts are printed."""
+    d0 = fits(dedup)[0]
+    if not np.any(d0['stratum'] == 3):
+        pytest.skip("fixture without the round-6 replication sample")
+    miss, miss_ref, pval = _envelope(dedup, sample='replication')
+    d, out, status, info, nlz_gpu, st = sub(*fits(dedup), ~base_cells(d0))
+    ref_fs = d['out8'][:, 0, 0]
+    rel = np.where(np.isfinite(out[:, 0]), np.abs(out[:, 0] - ref_fs) / np.abs(ref_fs), np.inf)
+    rel_ref = np.abs(d['out8'][:, 1:, 0] - ref_fs[:, None]) / np.abs(ref_fs[:, None])
+    k, expect, pord = order_test(rel > 1e-6, rel_ref > 1e-6)
+    mr, z = rank_test(info[:, 3], d['evals'])
+    r, lo, hi = eval_ratio(info[:, 3], d['evals'].astype(float).mean(1))
+    print(f"OI_DEDUP={dedup} replication ({len(rel)} cells): envelope misses GPU {len(miss)} vs held-out run "
+          f"{len(miss_ref)} (worst-of-6 P = {pval:.3f}); beyond 1e-6 GPU {np.mean(rel > 1e-6):.3f} vs reference "
+          f"{np.mean(rel_ref > 1e-6):.3f} (per run {np.round(np.mean(rel_ref > 1e-6, 0), 3).tolist()}), "
+          f"P(>= {k}) = {pord:.3f}; median fs rel-err {np.median(rel):.2e}; evaluations GPU/reference {r:.3f} "
+          f"[{lo:.3f} .. {hi:.3f}], rank z = {z:.2f}")
+    assert np.median(rel) <= 1e-8
+    assert pval >= 0.01 and pord >= 0.01 and abs(z) < 2.58, (pval, pord, z)
