@@ -277,9 +277,19 @@ __device__ __forceinline__ void mfma16x16(d4& acc, const double* Am, int la, boo
 #endif
 // stage timestamps for tools/diag_engine_probe (compiled in only there)
 #ifdef OI_DIAG_TIMING
+// sums of the stamps over every diagonal factor block 0 runs (slot 15: calls);
+// differences of consecutive sums = total cycles per stage
 __device__ long long g_diag_stamps[16];
 #define DIAG_STAMP(k) \
-  do { if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_stamps[k] = clock64(); } while (0)
+  do { if (threadIdx.x == 0 && blockIdx.x == 0) { g_diag_stamps[k] += clock64(); if (k == 0) g_diag_stamps[15] += 1; } } while (0)
+extern "C" int oi_diag_stamps(long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_stamps), sizeof(long long) * 16) != hipSuccess) return 1;
+  if (reset) {
+    long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_stamps), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
 #else
 #define DIAG_STAMP(k) do {} while (0)
 #endif
@@ -445,8 +455,12 @@ static_assert(DIAG_LDS <= GEMM2_LDS, "the diagonal factor must fit k_panel_even'
 static_assert(DIAG_LDS <= GEMM4_LDS, "the diagonal factor must fit k_panel4's LDS");
 
 // the body of k_diag_factor4w for cell c and tile j: 256 threads work, any
-// larger workgroup passes every barrier with them; `lds` holds DIAG_LDS doubles
-__device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds) {
+// larger workgroup passes every barrier with them; `lds` holds DIAG_LDS doubles.
+// in_lds (j > 0, the fused look-ahead of k_chol_panel / k_panel_even): the
+// caller left the updated tile in As already (row-major, stride DW_LD, zeros
+// above the diagonal -- the doubles the load below would read back), so it is
+// handed over without a store -> barrier -> load round trip through L2
+__device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds, bool in_lds = false) {
   double* As = lds;
   double* Vs = As + NB * DW_LD;
   SiteBlk* sb = (SiteBlk*)(Vs + 3 * NB);
@@ -513,7 +527,7 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds) {
   } else {
     // element (r, q) of the column-major tile at q*64 + r: 16 coalesced loads per
     // thread; the upper triangle (scratch of the look-ahead) is replaced by zeros
-    if (act)
+    if (act && !in_lds)
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int e = t + 256 * u, q = e >> 6, r = e & 63;
@@ -547,14 +561,6 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds) {
       const int e = t + 256 * u, q = e >> 6, r = e & 63;
       gst(Y + e, r >= q ? As[r * DW_LD + q] : 0.0);
     }
-  if (w == 0) {
-    double lg = (j * NB + lane < c.n) ? log(As[lane * (DW_LD + 1)]) : 0.0;
-    for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
-    if (lane == 0) {
-      const int ntile = c.T * (c.T + 1) / 2;
-      c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
-    }
-  }
   DIAG_STAMP(3);
   trtri4w(As, (double*)sb);  // (the j = 0 sites are dead by now)
   DIAG_STAMP(5);
@@ -591,6 +597,16 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds) {
       pp[0] = zz;
       pp[1] = zv;
       pp[2] = vv;
+    }
+  } else if (w == 1) {
+    // sum log L_rr: off wave 0's serial chain (the trtri leaves As's diagonal
+    // -- L's -- untouched; its inverse sits above it), beside the forward
+    // substitution
+    double lg = (j * NB + lane < c.n) ? log(As[lane * (DW_LD + 1)]) : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) lg += __shfl_down(lg, o, 64);
+    if (lane == 0) {
+      const int ntile = c.T * (c.T + 1) / 2;
+      c.part[OI_PART_LOGDET(ntile, c.T) + j] = lg;
     }
   }
   DIAG_STAMP(6);
@@ -807,8 +823,9 @@ __device__ __forceinline__ void post_left(const Quad& acc, double* lds, const do
 // GEN = (kbeg == 0): the column's A_ij are still pristine and generated here
 // (its own instantiation: the generating epilogue would cost the common
 // kbeg = j - 1 launches a wave per SIMD)
-template <bool GEN>
-__device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int x, double* lds, int fuse) {
+template <bool GEN, bool FUSE>
+__device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int x, double* lds) {
+  constexpr bool fuse = FUSE;
   const int T = c.T;
   if (j >= T || *c.status != OI_OK) return;
   const int ntrsm = T - 1 - j;
@@ -880,16 +897,36 @@ __device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int 
     stage_sites(c, i, sbd, threadIdx.x, 256);
     __syncthreads();
     const GenTile Ad = gen_tile(c, sbd, i, sbd, i);
+    if (fuse) {  // the diagonal tile j+1 is final: factor it here, handed over in LDS
+      double v[16];
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = acc1_row(mb, r), n = acc1_col(nb);
+            v[(2 * mb + nb) * 4 + r] = Ad(n, m) - accd.c[mb][nb][r];
+          }
+      __syncthreads();  // the staged sites are read
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = acc1_row(mb, r), n = acc1_col(nb);  // element (row n, column m)
+            lds[n * DW_LD + m] = n >= m ? v[(2 * mb + nb) * 4 + r] : 0.0;
+          }
+      diag_tile(c, i, lds, true);
+      return;
+    }
     for (int mb = 0; mb < 2; ++mb)
       for (int nb = 0; nb < 2; ++nb)
         for (int r = 0; r < 4; ++r) {
           const int m = acc1_row(mb, r), n = acc1_col(nb);
           gst(Yd + m * NB + n, Ad(n, m) - accd.c[mb][nb][r]);
         }
-    if (fuse) {  // the diagonal tile j+1 is final: factor it here
-      __syncthreads();
-      diag_tile(c, i, lds);
-    }
     return;
   }
   const int jj = x - ntrsm;
@@ -912,15 +949,15 @@ __device__ __forceinline__ void chol_slot(const OiCell& c, int j, int kbeg, int 
   alpha_update<256>(c, lds, XLD, jj, apre, lds + NB * XLD);  // alpha_jj += W_j,jj^T z_j
 }
 
-template <bool GEN>
+template <bool GEN, bool FUSE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_chol_panel(const OiCell* __restrict__ cells,
                                                    const int32_t* __restrict__ list, int j,
-                                                   int kbeg, int gx, int ncell, int fuse) {
+                                                   int kbeg, int gx, int ncell) {
   __shared__ __attribute__((aligned(16))) double lds[GEMM1_LDS];
   int ci, x;
   if (!xcd_cell_slot_lead0(gx, ncell, ci, x)) return;
-  chol_slot<GEN>(cells[list[ci]], j, kbeg, x, lds, fuse);
+  chol_slot<GEN, FUSE>(cells[list[ci]], j, kbeg, x, lds);
 }
 
 // --------------------------------------------------- k_panel_even(j), j even
@@ -960,8 +997,7 @@ __device__ __forceinline__ void emit_copy(const double* X, double* dst, int op, 
 // dst[n*64 + m] (op)= D_h[m][n] for the 64x64 half h of a gemm2 accumulator
 // (EMIT_GENSUB: dst = A - D_h, A the pristine tile generated by *gen).
 // Leaves the staged tile in X[n*XLD + m] (= dst's storage order) for reuse.
-__device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, double* dst, int op,
-                                          const GenTile* gen = nullptr) {
+__device__ __forceinline__ void stage_half(const Quad& acc, int h, double* X) {
   const int w = threadIdx.x >> 6;
   __syncthreads();
   if (((w & 3) >> 1) == h) {
@@ -971,6 +1007,10 @@ __device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, dou
           X[(acc_col(nb) - 64 * h) * XLD + acc_row(mb, r)] = acc.c[mb][nb][r];
   }
   __syncthreads();
+}
+__device__ __forceinline__ void emit_half(const Quad& acc, int h, double* X, double* dst, int op,
+                                          const GenTile* gen = nullptr) {
+  stage_half(acc, h, X);
   emit_copy(X, dst, op, gen);
 }
 
@@ -1049,10 +1089,15 @@ __device__ __forceinline__ void post_right(const Quad& acc, double* lds, const G
   __syncthreads();
 }
 
+// FUSE: the look-ahead slot factors the diagonal tile j+1 itself (its own
+// instantiation: with both hand-over paths in one kernel the register
+// allocator spilled)
+template <bool FUSE>
 __global__ __launch_bounds__(GEMM_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void k_panel_even(const OiCell* __restrict__ cells,
                                                             const int32_t* __restrict__ list,
-                                                            int j, int gx, int ncell, int fuse) {
+                                                            int j, int gx, int ncell) {
+  constexpr bool fuse = FUSE;
   __shared__ __attribute__((aligned(16))) double lds[GEMM2_LDS];
   __shared__ SiteBlk sb[3];  // sites of block row i, block columns j, j+1
   static_assert(NB * XLD <= GEMM2_LDS, "staging tile must fit the GEMM LDS");
@@ -1123,12 +1168,42 @@ void k_panel_even(const OiCell* __restrict__ cells,
         }
       }
     }
+    if (fuse) {
+      // the diagonal tile j+1 is final: factor it here, handed over in LDS.
+      // The two emit_half passes below, with A - acc kept in LDS and
+      // (A - acc) - L L^T formed in the lanes holding L L^T -- the doubles
+      // they would store and read back
+      const int wh = (threadIdx.x >> 6) & 3;
+      stage_half(acc, 1, lds);
+      for (int e = threadIdx.x; e < OI_TILE; e += GEMM_THREADS) {  // A - acc, in place
+        double* xe = lds + (e >> 6) * XLD + (e & 63);
+        *xe = Ai1(e & 63, e >> 6) - *xe;
+      }
+      __syncthreads();
+      if ((wh >> 1) == 1)  // the lanes holding L L^T: (A - acc) - L L^T at their own elements
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              lf.c[mb][nb][r] = lds[(acc_col(nb) - 64) * XLD + acc_row(mb, r)] - lf.c[mb][nb][r];
+      __syncthreads();
+      if ((wh >> 1) == 1)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = acc_row(mb, r), n = acc_col(nb) - 64;  // element (row m, column n)
+              lds[m * DW_LD + n] = m >= n ? lf.c[mb][nb][r] : 0.0;
+            }
+      diag_tile(c, i, lds, true);
+      return;
+    }
     emit_half(acc, 1, lds, tileL(c, i, i), EMIT_GENSUB, &Ai1);
     emit_half(lf, 1, lds, tileL(c, i, i), EMIT_SUB);  // (A_j+1,j+1 - acc) - L L^T
-    if (fuse) {  // the diagonal tile j+1 is final: factor it here
-      __syncthreads();
-      diag_tile(c, i, lds);
-    }
     return;
   }
   const int jj = x - ntrsm;
@@ -1798,12 +1873,16 @@ extern "C" int oi_launch_chol_panel(const OiCell* cells, const int32_t* list, in
                                     int j, int kbeg, int with_trtri, int fuse_diag, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
+  const dim3 g(grid1(gx, ncell));
   if (kbeg == 0)
-    hipLaunchKernelGGL(k_chol_panel<true>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, kbeg,
-                       gx, ncell, fuse_diag);
+    if (fuse_diag)
+      hipLaunchKernelGGL((k_chol_panel<true, true>), g, dim3(256), 0, S(stream), cells, list, j, kbeg, gx, ncell);
+    else
+      hipLaunchKernelGGL((k_chol_panel<true, false>), g, dim3(256), 0, S(stream), cells, list, j, kbeg, gx, ncell);
+  else if (fuse_diag)
+    hipLaunchKernelGGL((k_chol_panel<false, true>), g, dim3(256), 0, S(stream), cells, list, j, kbeg, gx, ncell);
   else
-    hipLaunchKernelGGL(k_chol_panel<false>, dim3(grid1(gx, ncell)), dim3(256), 0, S(stream), cells, list, j, kbeg,
-                       gx, ncell, fuse_diag);
+    hipLaunchKernelGGL((k_chol_panel<false, false>), g, dim3(256), 0, S(stream), cells, list, j, kbeg, gx, ncell);
   return ret();
 }
 
@@ -1811,8 +1890,12 @@ extern "C" int oi_launch_panel_even(const OiCell* cells, const int32_t* list, in
                                     int j, int with_trtri, int fuse_diag, void* stream) {
   const int gx = (maxT - 1 - j) + (with_trtri ? j : 0);
   if (ncell <= 0 || gx <= 0) return 0;
-  hipLaunchKernelGGL(k_panel_even, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j, gx,
-                     ncell, fuse_diag);
+  if (fuse_diag)
+    hipLaunchKernelGGL(k_panel_even<true>, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j,
+                       gx, ncell);
+  else
+    hipLaunchKernelGGL(k_panel_even<false>, dim3(grid1(gx, ncell)), dim3(GEMM_THREADS), 0, S(stream), cells, list, j,
+                       gx, ncell);
   return ret();
 }
 

@@ -1,8 +1,9 @@
 """Regenerate profiles/pmc_traffic.json (the `roofline.traffic` bench.py
 reports) from a pmc_summary.py output of the driver's command: HBM bytes per
 dispatch per kernel, under the names the library's profile uses
-(k_lauum_grad1 -> k_lauum_grad, k_chol_panel<false/true> -> k_chol_panel,
-dispatch-weighted; k_diag_factor4w -> k_diag_factor).  Kernels measured in
+(k_lauum_grad1 -> k_lauum_grad, every k_chol_panel<...> / k_panel_even<...>
+instantiation -> k_chol_panel / k_panel_even, dispatch-weighted;
+k_diag_factor4w -> k_diag_factor).  Kernels measured in
 earlier rounds and absent from this pass (k_svgp_train) keep their entries.
 Usage: python scripts/r06/pmc_traffic.py profiles/r06/final/pmc_hbm_summary.json"""
 import json
@@ -21,6 +22,9 @@ def main(path, out='profiles/pmc_traffic.json'):
     acc = {}
     for k, v in summ.items():
         name = ALIAS.get(k, k)
+        for tmpl in ('k_chol_panel', 'k_panel_even'):  # template instantiations
+            if name.startswith(f'void {tmpl}<'):
+                name = tmpl
         a = acc.setdefault(name, [0, 0.0, 0.0])
         a[0] += v['dispatches']
         a[1] += v['fetch_bytes_per_dispatch'] * v['dispatches']
