@@ -327,7 +327,14 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // upper triangle is scratch) on four waves, As <- L with zeros above the
 // diagonal.  Returns the smallest pivot in wave 0 (+inf in the other waves;
 // minNum passes a NaN pivot over, as the reference's cholesky does).
-__device__ __forceinline__ double potrf4w(double* As) {
+// Broadcasts (OI_POTRF_LDSB, round 6): the element the next column's pivot
+// waits for comes by v_readlane; the rest of column q (rows c0+q+2 ..) goes
+// through `bc` in LDS -- one store, then uniform-address reads, against two
+// v_readlane per element -- the same doubles in the same update order.
+#ifndef OI_POTRF_LDSB
+#define OI_POTRF_LDSB 1
+#endif
+__device__ __forceinline__ double potrf4w(double* As, double* bc) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = lane >> 4;
   double dmin = __builtin_inf();
 #pragma unroll
@@ -339,6 +346,7 @@ __device__ __forceinline__ double potrf4w(double* As) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) R[q] = As[r * DW_LD + c0 + q];
       // rows r < c0 + q compute values nobody reads (zeros are written back)
+      double bq[16], qprev = 0.0;  // column q-1's broadcast elements (rows c0+q+1 ..) and its qd
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int cc = c0 + q;
@@ -351,8 +359,25 @@ __device__ __forceinline__ double potrf4w(double* As) {
         const double l = d * il;
         const double qd = R[q] * il;
         R[q] = r == cc ? l : qd;
+        if (OI_POTRF_LDSB) {
+          // column q-1's updates of rows c0+q+1 .. (their broadcasts were read
+          // during this column's pivot), before column q's own updates of them
+          if (q >= 1 && q - 1 < 14)
 #pragma unroll
-        for (int s2 = q + 1; s2 < 16; ++s2) R[s2] -= qd * rdlane(R[q], c0 + s2);
+            for (int s2 = q + 1; s2 < 16; ++s2) R[s2] -= qprev * bq[s2];
+          if (q < 15) R[q + 1] -= qd * rdlane(R[q], c0 + q + 1);
+          if (q < 14) {
+            double* bb = bc + 64 * (q & 1);
+            bb[r] = R[q];
+#pragma unroll
+            for (int s2 = q + 2; s2 < 16; ++s2) bq[s2] = bb[c0 + s2];
+          }
+          qprev = qd;
+          __builtin_amdgcn_sched_barrier(0);  // (later columns' broadcasts not hoisted: registers)
+        } else {
+#pragma unroll
+          for (int s2 = q + 1; s2 < 16; ++s2) R[s2] -= qd * rdlane(R[q], c0 + s2);
+        }
       }
 #pragma unroll
       for (int q = 0; q < 16; ++q) As[r * DW_LD + c0 + q] = r >= c0 + q ? R[q] : 0.0;
@@ -541,7 +566,7 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds, b
   }
   lds_barrier();
   DIAG_STAMP(1);
-  const double dmin = potrf4w(As);  // smallest pivot (wave 0)
+  const double dmin = potrf4w(As, (double*)sb);  // smallest pivot (wave 0); sb: the broadcast scratch
   DIAG_STAMP(2);
   if (t == 0) bad = dmin <= 0.0;
   lds_barrier();
