@@ -304,8 +304,9 @@ extern "C" int oi_diag_stamps(long long* out, int reset) {
 // latency (config 1's lone cell waits for four of these per evaluation; the
 // round-2 single-wave kernel spent half its 60 k cycles outside the serial
 // potrf -- retired in round 4 with the round-1 kernel):
-//   potrf: 16-column panels; wave 0 factors the panel (row per lane, column
-//          values by v_readlane), all four waves then apply the trailing
+//   potrf: 16-column panels; wave 0 factors the panel (row per lane; the
+//          next pivot's column value by v_readlane, the rest of the column
+//          through LDS one column late), all four waves then apply the trailing
 //          update A_IK -= P_I P_K^T (I >= K > J) on v_mfma_f64_16x16x4f64;
 //   inverse: wave b inverts diagonal block b by forward substitution, one
 //          lane per column (L read by LDS broadcast), then the off-diagonal
