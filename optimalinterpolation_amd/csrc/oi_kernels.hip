@@ -472,8 +472,9 @@ __device__ __forceinline__ void trtri4w(double* As, double* dump) {
   }
 }
 
-// LDS of the diagonal factor: As (packed L / Inv) | Vs | sites (j = 0) | bad
-#define DIAG_LDS (NB * DW_LD + 3 * NB + 4 * NB + 2)
+// LDS of the diagonal factor: As (packed L / Inv) | Vs | sites (j = 0) | bad |
+// (the chains' partials: sb's 4 NB and 4 NB more)
+#define DIAG_LDS (NB * DW_LD + 3 * NB + 4 * NB + 2 + 4 * NB)
 // diag_tile(j + 1) runs inside the panel kernels on their GEMM LDS arrays
 // (the fused look-ahead factor, oi_engine.cpp OI_FUSE_DIAG_MIN)
 static_assert(DIAG_LDS <= GEMM1_LDS, "the diagonal factor must fit k_chol_panel's LDS");
@@ -599,16 +600,30 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds, b
       gst(Dj + e, inv_get(As, r, q));
     }
   // forward substitution, block j: z_j = Dinv_jj z_j (the panels subtracted the
-  // sum over k < j), v_j likewise for predict; z^T z, z^T v, v^T v partials
-  if (w == 0) {
-    double zp[4] = {0.0, 0.0, 0.0, 0.0}, vp[4] = {0.0, 0.0, 0.0, 0.0};  // four chains
-#pragma unroll 8  // (full unrolling hoists all 64 packed reads: 255 VGPRs; 8 and 16 measured equal)
-    for (int q = 0; q < NB; ++q) {
+  // sum over k < j), v_j likewise for predict; z^T z, z^T v, v^T v partials.
+  // Four chains, q = k (mod 4), summed (c0 + c1) + (c2 + c3): chain k on wave k
+  // (round 6; the round-5 kernel ran the four interleaved on wave 0 -- the same
+  // operations in the same order), the partials through LDS (sb is dead: the
+  // sites, the potrf broadcasts and the inverse's scratch are done).  For a
+  // fitting cell v = 0: its chains are skipped (they summed +0 exactly)
+  double* Pz = (double*)sb;  // 4 x NB
+  double* Pv = Vs + 7 * NB + 2;  // 4 x NB, past `bad`
+  if (w < 4) {
+    double zp = 0.0, vp = 0.0;
+#pragma unroll 4
+    for (int i = 0; i < NB / 4; ++i) {
+      const int q = 4 * i + w;
       const double a = inv_get(As, lane, q);
-      zp[q & 3] = fma(a, Vs[q], zp[q & 3]);
-      vp[q & 3] = fma(a, Vs[NB + q], vp[q & 3]);
+      zp = fma(a, Vs[q], zp);
+      if (pred) vp = fma(a, Vs[NB + q], vp);
     }
-    const double zn = (zp[0] + zp[1]) + (zp[2] + zp[3]), vn = (vp[0] + vp[1]) + (vp[2] + vp[3]);
+    Pz[w * NB + lane] = zp;
+    if (pred) Pv[w * NB + lane] = vp;
+  }
+  lds_barrier();
+  if (w == 0) {
+    const double zn = (Pz[lane] + Pz[NB + lane]) + (Pz[2 * NB + lane] + Pz[3 * NB + lane]);
+    const double vn = pred ? (Pv[lane] + Pv[NB + lane]) + (Pv[2 * NB + lane] + Pv[3 * NB + lane]) : 0.0;
     gst(zj + lane, zn);
     if (pred) gst(vj + lane, vn);
     Vs[2 * NB + lane] = zn;
@@ -645,13 +660,19 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds, b
         const int e = t + 256 * u;
         gst(Wj + e, inv_get(As, e >> 6, e & 63));
       }
-    lds_barrier();  // z_j in Vs
-    if (w == 0) {
-      double ap[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-      for (int q = 0; q < NB; ++q) ap[q & 3] = fma(inv_get(As, q, lane), Vs[2 * NB + q], ap[q & 3]);
-      gst(c.vec + c.T * NB + j * NB + lane, (ap[0] + ap[1]) + (ap[2] + ap[3]));
+    lds_barrier();  // z_j in Vs (and wave 0 done with Pz)
+    if (w < 4) {  // alpha's four chains likewise, chain k on wave k
+      double ap = 0.0;
+#pragma unroll 4
+      for (int i = 0; i < NB / 4; ++i) {
+        const int q = 4 * i + w;
+        ap = fma(inv_get(As, q, lane), Vs[2 * NB + q], ap);
+      }
+      Pz[w * NB + lane] = ap;
     }
+    lds_barrier();
+    if (w == 0)
+      gst(c.vec + c.T * NB + j * NB + lane, (Pz[lane] + Pz[NB + lane]) + (Pz[2 * NB + lane] + Pz[3 * NB + lane]));
   }
   DIAG_STAMP(7);
 }
