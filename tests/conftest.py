@@ -39,7 +39,16 @@ def _blas_default_threads(request):
         yield
         return
     from threadpoolctl import threadpool_limits
-    with threadpool_limits(_BLAS_DEFAULT):
+    # one such test at a time across the workers: two full OpenBLAS pools on
+    # the same CPUs spin against each other (test_gpr3d_bitwise: 9 s alone,
+    # ~575 s beside test_cg_trace_bitwise under -n 4)
+    try:
+        from filelock import FileLock
+        lock = FileLock(os.path.join(os.environ.get('TMPDIR', '/tmp'), 'oi_blas_default_tests.lock'))
+    except ImportError:
+        import contextlib
+        lock = contextlib.nullcontext()
+    with lock, threadpool_limits(_BLAS_DEFAULT):
         yield
 
 
