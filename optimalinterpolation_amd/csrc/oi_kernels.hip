@@ -335,7 +335,10 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 #ifndef OI_POTRF_LDSB
 #define OI_POTRF_LDSB 1
 #endif
-__device__ __forceinline__ double potrf4w(double* As, double* bc) {
+// Y (optional): the tile's global storage -- panel J-1's columns of L, final,
+// are stored by waves 1-3 while wave 0 factors panel J (the last panel's by
+// the caller), instead of all 64 columns after the factorisation
+__device__ __forceinline__ double potrf4w(double* As, double* bc, double* Y = nullptr) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = lane >> 4;
   double dmin = __builtin_inf();
 #pragma unroll
@@ -382,6 +385,15 @@ __device__ __forceinline__ double potrf4w(double* As, double* bc) {
       }
 #pragma unroll
       for (int q = 0; q < 16; ++q) As[r * DW_LD + c0 + q] = r >= c0 + q ? R[q] : 0.0;
+    } else if (Y && w < 4 && J >= 1) {
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {  // 16 columns x 64 rows over 192 lanes; column-major, zeros above
+        const int e = (w - 1) * 64 + lane + 192 * u;
+        if (u < 5 || e < 1024) {
+          const int q = 16 * (J - 1) + (e >> 6), r = e & 63;
+          gst(Y + q * NB + r, r >= q ? As[r * DW_LD + q] : 0.0);
+        }
+      }
     }
     lds_barrier();
     if (J == 3) break;
@@ -568,7 +580,7 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds, b
   }
   lds_barrier();
   DIAG_STAMP(1);
-  const double dmin = potrf4w(As, (double*)sb);  // smallest pivot (wave 0); sb: the broadcast scratch
+  const double dmin = potrf4w(As, (double*)sb, Y);  // smallest pivot (wave 0); sb: the broadcast scratch
   DIAG_STAMP(2);
   if (t == 0) bad = dmin <= 0.0;
   lds_barrier();
@@ -581,11 +593,11 @@ __device__ __forceinline__ void diag_tile(const OiCell& c, int j, double* lds, b
     }
     return;
   }
-  // L_jj (column-major) and sum log L_rr
+  // L_jj (column-major): columns 0-47 went out during the potrf, the last panel's here
   if (act)
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = t + 256 * u, q = e >> 6, r = e & 63;
+    for (int u = 0; u < 4; ++u) {
+      const int e = 48 * NB + t + 256 * u, q = e >> 6, r = e & 63;
       gst(Y + e, r >= q ? As[r * DW_LD + q] : 0.0);
     }
   DIAG_STAMP(3);
